@@ -1,0 +1,242 @@
+"""acquire-zarr MI355X multiscale downsampler — Python binding of the C ABI.
+
+The product is the native library ``libaqz_downsampler.so`` (HIP kernels for
+gfx950 + the C ABI declared in ``include/aqz_downsampler.h`` + the C++
+``aqz::Downsampler`` mirror of the reference's ``zarr::Downsampler``).  This
+module is a thin ctypes binding used by the tests and ``bench.py``; it never
+computes anything itself and raises if the native library is missing — there
+is no CPU fallback.
+
+Import it as ``acquire_zarr_amd`` (see ``aqz_pkg.py`` at the repo root; the
+directory name carries a hyphen).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libaqz_downsampler.so")
+
+# ZarrDataType (zarr.types.h:55-68), ZarrDownsamplingMethod (:90-97),
+# ZarrDimensionType (:81-88) numeric values.
+NP_DTYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16,
+             np.int32, np.int64, np.float32, np.float64]
+DECIMATE, MEAN, MIN, MAX = 0, 1, 2, 3
+SPACE, CHANNEL, TIME, OTHER = 0, 1, 2, 3
+METHODS = {"decimate": DECIMATE, "mean": MEAN, "min": MIN, "max": MAX}
+
+# C ABI symbols (include/aqz_downsampler.h); the not-GPU test checks the
+# library exports exactly these.
+EXPORTS = (
+    "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
+    "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
+    "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
+    "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
+    "aqz_method_metadata_json", "aqz_version",
+)
+
+
+class AqzError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{message} (status {status})")
+        self.status = status
+
+
+class Dimension(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32),
+                ("array_size_px", ctypes.c_uint32),
+                ("chunk_size_px", ctypes.c_uint32),
+                ("shard_size_chunks", ctypes.c_uint32),
+                ("scale", ctypes.c_double)]
+
+
+class LevelDesc(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32),
+                ("height", ctypes.c_uint32),
+                ("planes", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the native library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C acquire-zarr_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+    L.aqz_plan_levels.argtypes = [ctypes.POINTER(Dimension), u32, u32,
+                                  ctypes.POINTER(Dimension), u32, ctypes.POINTER(u32)]
+    L.aqz_ds_create.argtypes = [ctypes.POINTER(LevelDesc), u32, i32, i32, i32,
+                                ctypes.POINTER(vp)]
+    L.aqz_ds_destroy.argtypes = [vp]
+    L.aqz_ds_destroy.restype = None
+    L.aqz_ds_add_frame.argtypes = [vp, vp, sz]
+    L.aqz_ds_add_device_frame.argtypes = [vp, vp, sz]
+    L.aqz_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz),
+                                    ctypes.POINTER(i32)]
+    L.aqz_ds_run_device_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
+                                          ctypes.POINTER(u32), vp]
+    L.aqz_ds_level_bytes.argtypes = [vp, u32]
+    L.aqz_ds_level_bytes.restype = sz
+    L.aqz_ds_level_count.argtypes = [vp]
+    L.aqz_ds_level_count.restype = u32
+    L.aqz_ds_device_memory_usage.argtypes = [vp]
+    L.aqz_ds_device_memory_usage.restype = sz
+    L.aqz_ds_last_error.argtypes = [vp]
+    L.aqz_ds_last_error.restype = ctypes.c_char_p
+    L.aqz_last_error.argtypes = []
+    L.aqz_last_error.restype = ctypes.c_char_p
+    L.aqz_method_name.argtypes = [i32]
+    L.aqz_method_name.restype = ctypes.c_char_p
+    L.aqz_method_metadata_json.argtypes = [i32]
+    L.aqz_method_metadata_json.restype = ctypes.c_char_p
+    L.aqz_version.argtypes = []
+    L.aqz_version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def dtype_code(dt) -> int:
+    name = np.dtype(dt).name
+    for i, t in enumerate(NP_DTYPES):
+        if np.dtype(t).name == name:
+            return i
+    raise ValueError(f"unsupported dtype {dt}")
+
+
+def plan_levels(dims, max_levels: int = 0):
+    """Level planner (make_writer_configurations_, downsampler.cpp:493-597).
+
+    `dims`: storage-order (type, size, chunk, shard[, scale]) tuples; a 2-D
+    list gets the reference's phantom singleton dimension prepended
+    (array.dimensions.cpp:149-152).  Returns one list of tuples per level.
+    """
+    dims = list(dims)
+    if len(dims) == 2:
+        dims = [(OTHER, 1, 1, 1, 1.0)] + dims
+    nd = len(dims)
+    arr = (Dimension * nd)(*[Dimension(d[0], d[1], d[2], d[3],
+                                       d[4] if len(d) > 4 else 1.0) for d in dims])
+    n = ctypes.c_uint32(0)
+    L = lib()
+    rc = L.aqz_plan_levels(arr, nd, max_levels, None, 0, ctypes.byref(n))
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+    out = (Dimension * (nd * n.value))()
+    rc = L.aqz_plan_levels(arr, nd, max_levels, out, n.value, ctypes.byref(n))
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+    return [[(o.type, o.array_size_px, o.chunk_size_px, o.shard_size_chunks, o.scale)
+             for o in out[l * nd:(l + 1) * nd]] for l in range(n.value)]
+
+
+def level_geometry(levels):
+    """(width, height, planes) per level, as add_frame reads them."""
+    return [(lv[-1][1], lv[-2][1], lv[-3][1]) for lv in levels]
+
+
+def method_name(method: int):
+    r = lib().aqz_method_name(method)
+    return None if r is None else r.decode()
+
+
+def method_metadata(method: int):
+    import json
+    r = lib().aqz_method_metadata_json(method)
+    return None if r is None else json.loads(r.decode())
+
+
+class Downsampler:
+    """Binding of one ``aqz_ds`` handle: the GPU replacement of
+    ``zarr::Downsampler`` (downsampler.hh:11-64).
+
+    ``geometry`` is the per-level (width, height, planes) list (see
+    ``level_geometry(plan_levels(...))``).
+    """
+
+    def __init__(self, geometry, dtype, method: int, device: int = -1):
+        self.dtype = np.dtype(dtype)
+        self.geometry = [tuple(int(x) for x in g) for g in geometry]
+        n = len(self.geometry)
+        desc = (LevelDesc * n)(*[LevelDesc(*g) for g in self.geometry])
+        h = ctypes.c_void_p()
+        L = lib()
+        rc = L.aqz_ds_create(desc, n, dtype_code(self.dtype), method, device,
+                             ctypes.byref(h))
+        if rc:
+            raise AqzError(rc, L.aqz_last_error().decode())
+        self._h = h
+        self.method = method
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib().aqz_ds_destroy(h)
+        self._h = None
+
+    __del__ = close
+
+    def _check(self, rc):
+        if rc:
+            raise AqzError(rc, lib().aqz_ds_last_error(self._h).decode())
+
+    @property
+    def n_levels(self) -> int:
+        return len(self.geometry)
+
+    def level_bytes(self, level: int) -> int:
+        return lib().aqz_ds_level_bytes(self._h, level)
+
+    def device_memory_usage(self) -> int:
+        return lib().aqz_ds_device_memory_usage(self._h)
+
+    def add_frame(self, frame: np.ndarray):
+        frame = np.ascontiguousarray(frame)
+        if frame.dtype != self.dtype:
+            raise TypeError(f"frame dtype {frame.dtype} != {self.dtype}")
+        self._check(lib().aqz_ds_add_frame(self._h, frame.ctypes.data, frame.nbytes))
+
+    def add_device_frame(self, device_ptr: int, nbytes: int):
+        self._check(lib().aqz_ds_add_device_frame(self._h, device_ptr, nbytes))
+
+    def take_frame(self, level: int):
+        """Cached frame of `level` as an (h, w) array, or None."""
+        w, h, _ = self.geometry[level] if 0 <= level < self.n_levels else (0, 0, 0)
+        out = np.empty((max(h, 1), max(w, 1)), dtype=self.dtype)
+        nb = ctypes.c_size_t(0)
+        has = ctypes.c_int(0)
+        self._check(lib().aqz_ds_take_frame(self._h, level, out.ctypes.data,
+                                            out.nbytes, ctypes.byref(nb),
+                                            ctypes.byref(has)))
+        return out if has.value else None
+
+    def run_device_batch(self, device_frames: int, n_frames: int, device_outs,
+                         stream: int = 0):
+        """Device-resident batch: `device_outs[L]` are device pointers
+        (index 0 ignored).  Returns frames emitted per level."""
+        n = self.n_levels
+        outs = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in device_outs])
+        counts = (ctypes.c_uint32 * n)()
+        self._check(lib().aqz_ds_run_device_batch(
+            self._h, device_frames, n_frames, outs, counts,
+            ctypes.c_void_p(stream) if stream else None))
+        return list(counts)
+
+
+def alg_bytes_per_frame(geometry, bpp: int) -> int:
+    """Algorithmic HBM bytes per 2-D frame: read level 0 once, write every
+    output level once."""
+    w0, h0, _ = geometry[0]
+    total = w0 * h0 * bpp
+    for w, h, _ in geometry[1:]:
+        total += w * h * bpp
+    return total

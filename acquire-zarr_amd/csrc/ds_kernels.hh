@@ -1,0 +1,82 @@
+// ds_kernels.hh — launchers for the MI355X pyramid kernels (ds_kernels.hip).
+//
+// Three kernels cover the reference's two hot loops
+// (src/streaming/downsampler.cpp):
+//   * cascade   — scale_image<T> (:139-206) applied 1..4 times in one pass:
+//                 each wave reads a 2^NL-row base tile once and writes every
+//                 level of the run; odd edges replicated per level.
+//   * xy_generic — one scale_image<T> level, one output pixel per lane; the
+//                 fallback for widths the vector path cannot tile.
+//   * zpair     — average_two_frames<T> (:208-246), out = f(earlier, current).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace aqz {
+
+constexpr int kMaxFusedLevels = 4;
+
+// One output level of a cascade launch.  `frame_elems` is the element stride
+// between consecutive frames of that level (w*h for densely packed batches).
+struct LevelOut
+{
+    void* ptr;
+    uint64_t frame_elems;
+    uint32_t w, h;
+};
+
+size_t dtype_bytes(int dtype);
+bool dtype_valid(int dtype);
+bool method_valid(int method);
+
+// True when the fused vector cascade can run the given run of levels: the
+// input width must be a multiple of the per-lane vector (16 bytes of T), all
+// pointers 16-byte aligned and each output level exactly ceil(in/2).
+bool cascade_supported(int dtype,
+                       const void* src,
+                       uint32_t W,
+                       uint32_t H,
+                       const LevelOut* outs,
+                       int n_out);
+
+// Fused multi-level XY reduction of `n_frames` frames (frame i at
+// src + i*src_frame_elems).  n_out in [1, kMaxFusedLevels].
+hipError_t launch_cascade(int dtype,
+                          int method,
+                          const void* src,
+                          uint64_t src_frame_elems,
+                          uint32_t W,
+                          uint32_t H,
+                          const LevelOut* outs,
+                          int n_out,
+                          uint32_t n_frames,
+                          hipStream_t stream);
+
+// One XY level, any width/alignment.
+hipError_t launch_xy_generic(int dtype,
+                             int method,
+                             const void* src,
+                             uint64_t src_frame_elems,
+                             uint32_t w,
+                             uint32_t h,
+                             const LevelOut& out,
+                             uint32_t n_frames,
+                             hipStream_t stream);
+
+// out[i] = reduce2(earlier[i], current[i]) over n elements; `out` may alias
+// either input.
+hipError_t launch_zpair(int dtype,
+                        int method,
+                        void* out,
+                        const void* earlier,
+                        const void* current,
+                        uint64_t n,
+                        hipStream_t stream);
+
+// Tuning knob for the cascade grid (waves resident per CU × CUs); 0 = auto.
+void set_cascade_grid_cap(uint32_t blocks);
+
+} // namespace aqz

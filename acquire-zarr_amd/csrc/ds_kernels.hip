@@ -1,0 +1,650 @@
+// ds_kernels.hip — CDNA4 (gfx950) kernels for the acquire-zarr multiscale
+// pyramid.  See ds_kernels.hh for the contract and DESIGN.md for the
+// roofline analysis.
+//
+// Semantics restated from acquire-zarr v0.8.1 src/streaming/downsampler.cpp:
+//   reducers        :39-137 (decimate/mean/min/max, 4- and 2-operand forms)
+//   scale_image<T>  :139-206 (2x2 reduce, odd right/bottom edge replicated)
+//   average_two_frames<T> :208-246 (dst = f(earlier, current))
+// The arithmetic is bit-exact with the reference binary: narrow integers are
+// promoted to int, 32/64-bit integer sums wrap, floats sum left to right and
+// divide by 4 (exact as a multiply by 0.25), min/max are compare-select
+// chains seeded with the first operand so NaN order matches.
+//
+// Design: this is an HBM-bound stencil, not a contraction — no MFMA, no LDS
+// staging.  Each wave owns a tile of 64 lanes x 16 bytes wide and 2^NL rows
+// tall, issues all 2^NL row loads (16 B per lane, 1 KiB per wave
+// instruction) before any arithmetic, and reduces the pyramid in registers:
+// in-lane while a lane still holds >= 2 columns of a level, then across lanes
+// with __shfl_down at doubling strides.  Every level of the run is written
+// from the same pass, so the base frame is read exactly once.
+#include "ds_kernels.hh"
+
+#include <type_traits>
+
+namespace aqz {
+namespace {
+
+// Native 16-byte vector (HIP's uint4 is a struct; the builtins want this).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+enum
+{
+    kDecimate = 0,
+    kMean = 1,
+    kMin = 2,
+    kMax = 3
+};
+
+// ---- reducers --------------------------------------------------------------
+
+template<typename T>
+__device__ __forceinline__ T
+mean4(T a, T b, T c, T d)
+{
+    if constexpr (std::is_floating_point_v<T>) {
+        return (((a + b) + c) + d) / T(4);
+    } else if constexpr (sizeof(T) < sizeof(int)) {
+        return T((int(a) + int(b) + int(c) + int(d)) / 4);
+    } else {
+        using U = std::make_unsigned_t<T>;
+        const T s = T(U(a) + U(b) + U(c) + U(d));
+        return T(s / T(4));
+    }
+}
+
+template<typename T>
+__device__ __forceinline__ T
+mean2(T a, T b)
+{
+    if constexpr (std::is_floating_point_v<T>) {
+        return (a + b) / T(2);
+    } else if constexpr (sizeof(T) < sizeof(int)) {
+        return T((int(a) + int(b)) / 2);
+    } else {
+        using U = std::make_unsigned_t<T>;
+        const T s = T(U(a) + U(b));
+        return T(s / T(2));
+    }
+}
+
+template<typename T, int M>
+__device__ __forceinline__ T
+reduce4(T a, T b, T c, T d)
+{
+    if constexpr (M == kDecimate) {
+        return a;
+    } else if constexpr (M == kMean) {
+        return mean4(a, b, c, d);
+    } else if constexpr (M == kMin) {
+        T v = a;
+        v = (b < v) ? b : v;
+        v = (c < v) ? c : v;
+        v = (d < v) ? d : v;
+        return v;
+    } else {
+        T v = a;
+        v = (b > v) ? b : v;
+        v = (c > v) ? c : v;
+        v = (d > v) ? d : v;
+        return v;
+    }
+}
+
+template<typename T, int M>
+__device__ __forceinline__ T
+reduce2(T a, T b)
+{
+    if constexpr (M == kDecimate) {
+        return a;
+    } else if constexpr (M == kMean) {
+        return mean2(a, b);
+    } else if constexpr (M == kMin) {
+        return a < b ? a : b;
+    } else {
+        return a > b ? a : b;
+    }
+}
+
+// ---- cross-lane move of any 1/2/4/8-byte element ---------------------------
+
+template<typename T>
+__device__ __forceinline__ T
+shfl_down_any(T v, int delta)
+{
+    if constexpr (sizeof(T) <= 4) {
+        uint32_t x = 0;
+        __builtin_memcpy(&x, &v, sizeof(T));
+        x = __shfl_down(x, (unsigned)delta);
+        T r;
+        __builtin_memcpy(&r, &x, sizeof(T));
+        return r;
+    } else {
+        unsigned long long x;
+        __builtin_memcpy(&x, &v, 8);
+        x = __shfl_down(x, (unsigned)delta);
+        T r;
+        __builtin_memcpy(&r, &x, 8);
+        return r;
+    }
+}
+
+// Store N contiguous elements of T as one naturally aligned access.
+template<typename T, int N>
+__device__ __forceinline__ void
+store_vec(T* dst, const T (&v)[N])
+{
+    constexpr int B = int(sizeof(T)) * N;
+    static_assert(B == 1 || B == 2 || B == 4 || B == 8 || B == 16, "width");
+    if constexpr (B == 16) {
+        u32x4 q;
+        __builtin_memcpy(&q, v, 16);
+        *reinterpret_cast<u32x4*>(dst) = q;
+    } else if constexpr (B == 8) {
+        uint64_t q;
+        __builtin_memcpy(&q, v, 8);
+        *reinterpret_cast<uint64_t*>(dst) = q;
+    } else if constexpr (B == 4) {
+        uint32_t q;
+        __builtin_memcpy(&q, v, 4);
+        *reinterpret_cast<uint32_t*>(dst) = q;
+    } else if constexpr (B == 2) {
+        uint16_t q;
+        __builtin_memcpy(&q, v, 2);
+        *reinterpret_cast<uint16_t*>(dst) = q;
+    } else {
+        *reinterpret_cast<uint8_t*>(dst) = *reinterpret_cast<const uint8_t*>(v);
+    }
+}
+
+// ---- fused cascade ---------------------------------------------------------
+
+struct CascadeParams
+{
+    const uint8_t* src;
+    uint64_t src_frame_elems;
+    uint32_t W, H;         // input level geometry
+    uint32_t units_x;      // column tiles per frame
+    uint32_t units_y;      // row tiles per frame
+    uint32_t total_units;  // units_x * units_y * n_frames
+    uint8_t* dst[kMaxFusedLevels];
+    uint64_t dst_frame_elems[kMaxFusedLevels];
+    uint32_t w[kMaxFusedLevels];
+    uint32_t h[kMaxFusedLevels];
+};
+
+// Level J (1-based within the run) from level J-1 held in registers as
+// RI rows x CI columns per lane.  CI == 1 means the lane holds one column of
+// a column group spread over SI lanes (only the group's first lane is
+// meaningful); the right-hand neighbour then comes from lane + SI.
+template<typename T, int M, int J, int NL, int RI, int CI, bool EDGE>
+__device__ __forceinline__ void
+cascade_level(const CascadeParams& p,
+              const T (&in)[RI][CI],
+              uint32_t f,
+              uint32_t row0,
+              uint32_t col0,
+              int lane)
+{
+    constexpr int C = 16 / int(sizeof(T));
+    constexpr int RO = RI / 2;
+    constexpr bool kInLane = CI >= 2;
+    constexpr int CO = kInLane ? CI / 2 : 1;
+    constexpr int SI = ((1 << (J - 1)) >= C) ? ((1 << (J - 1)) / C) : 1;
+    constexpr int SO = ((1 << J) >= C) ? ((1 << J) / C) : 1;
+
+    const uint32_t win = (J == 1) ? p.W : p.w[J - 2];
+    const uint32_t hin = (J == 1) ? p.H : p.h[J - 2];
+    const uint32_t cin0 = col0 >> (J - 1);
+    const uint32_t rin0 = row0 >> (J - 1);
+
+    T out[RO][CO];
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+#pragma unroll
+        for (int c = 0; c < CO; ++c) {
+            T here, right, down, diag;
+            if constexpr (kInLane) {
+                here = in[2 * r][2 * c];
+                right = in[2 * r][2 * c + 1];
+                down = in[2 * r + 1][2 * c];
+                diag = in[2 * r + 1][2 * c + 1];
+            } else {
+                here = in[2 * r][0];
+                down = in[2 * r + 1][0];
+                right = shfl_down_any(here, SI);
+                diag = shfl_down_any(down, SI);
+            }
+            if constexpr (EDGE) {
+                // scale_image edge replication (downsampler.cpp:186-197):
+                // last column of an odd width / last row of an odd height.
+                const uint32_t col = cin0 + (kInLane ? 2u * c : 0u);
+                const bool pw = col + 1 >= win;
+                const bool ph = rin0 + 2u * r + 1 >= hin;
+                const T r_ = pw ? here : right;
+                const T g_ = ph ? r_ : (pw ? down : diag);
+                const T d_ = ph ? here : down;
+                right = r_;
+                down = d_;
+                diag = g_;
+            }
+            out[r][c] = reduce4<T, M>(here, right, down, diag);
+        }
+    }
+
+    const uint32_t wout = p.w[J - 1];
+    const uint32_t hout = p.h[J - 1];
+    const uint32_t cout0 = col0 >> J;
+    const uint32_t rout0 = row0 >> J;
+    const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
+    T* dst = reinterpret_cast<T*>(p.dst[J - 1]) +
+             uint64_t(f) * p.dst_frame_elems[J - 1];
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+        bool ok = leader;
+        if constexpr (EDGE) {
+            ok = ok && (rout0 + r < hout) && (cout0 < wout);
+        }
+        if (ok) {
+            store_vec<T, CO>(dst + uint64_t(rout0 + r) * wout + cout0, out[r]);
+        }
+    }
+
+    if constexpr (J < NL) {
+        cascade_level<T, M, J + 1, NL, RO, CO, EDGE>(p, out, f, row0, col0, lane);
+    }
+}
+
+template<typename T, int M, int NL, bool EDGE>
+__device__ __forceinline__ void
+cascade_unit(const CascadeParams& p,
+             uint32_t f,
+             uint32_t row0,
+             uint32_t col0,
+             int lane)
+{
+    constexpr int C = 16 / int(sizeof(T));
+    constexpr int R = 1 << NL;
+    const T* src =
+      reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
+
+    T v[R][C];
+    // All row loads are issued before any arithmetic: 2^NL outstanding
+    // 16-byte loads per lane (1 KiB per wave instruction).
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bool ok = true;
+        if constexpr (EDGE) {
+            ok = (row0 + r < p.H) && (col0 < p.W);
+        }
+        u32x4 q = { 0u, 0u, 0u, 0u };
+        if (ok) {
+            q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+              src + uint64_t(row0 + r) * p.W + col0));
+        }
+        __builtin_memcpy(&v[r][0], &q, 16);
+    }
+    cascade_level<T, M, 1, NL, R, C, EDGE>(p, v, f, row0, col0, lane);
+}
+
+template<typename T, int M, int NL>
+__global__ __launch_bounds__(256) void
+cascade_kernel(CascadeParams p)
+{
+    constexpr int C = 16 / int(sizeof(T));
+    constexpr int R = 1 << NL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave_in_block =
+      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t waves_per_block = blockDim.x >> 6;
+    const uint32_t nwaves = gridDim.x * waves_per_block;
+
+    for (uint32_t u = blockIdx.x * waves_per_block + wave_in_block;
+         u < p.total_units;
+         u += nwaves) {
+        const uint32_t ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        const uint32_t uy = t % p.units_y;
+        const uint32_t f = t / p.units_y;
+        const uint32_t row0 = uy * R;
+        const uint32_t tile_col0 = ux * (64u * C);
+        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+        const bool interior =
+          (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
+        if (interior) {
+            cascade_unit<T, M, NL, false>(p, f, row0, col0, lane);
+        } else {
+            cascade_unit<T, M, NL, true>(p, f, row0, col0, lane);
+        }
+    }
+}
+
+// ---- generic single level --------------------------------------------------
+
+template<typename T, int M>
+__global__ __launch_bounds__(256) void
+xy_generic_kernel(const T* __restrict__ src,
+                  uint64_t src_frame_elems,
+                  uint32_t w,
+                  uint32_t h,
+                  T* __restrict__ dst,
+                  uint64_t dst_frame_elems,
+                  uint32_t wo,
+                  uint32_t ho,
+                  uint64_t total)
+{
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+         i += uint64_t(gridDim.x) * blockDim.x) {
+        const uint32_t c = uint32_t(i % wo);
+        const uint64_t t = i / wo;
+        const uint32_t r = uint32_t(t % ho);
+        const uint64_t f = t / ho;
+        const uint32_t col = 2 * c, row = 2 * r;
+        const bool pw = col + 1 >= w;
+        const bool ph = row + 1 >= h;
+        const T* s = src + f * src_frame_elems + uint64_t(row) * w + col;
+        const uint32_t dr = pw ? 0 : 1;
+        const uint64_t dd = ph ? 0 : w;
+        const T here = s[0];
+        const T right = s[dr];
+        const T down = s[dd];
+        const T diag = s[dd + dr];
+        dst[f * dst_frame_elems + uint64_t(r) * wo + c] =
+          reduce4<T, M>(here, right, down, diag);
+    }
+}
+
+// ---- Z pair ----------------------------------------------------------------
+
+template<typename T, int M>
+__global__ __launch_bounds__(256) void
+zpair_kernel(T* out, const T* earlier, const T* current, uint64_t n)
+{
+    constexpr int C = 16 / int(sizeof(T));
+    const uint64_t nvec = n / C;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < nvec; i += stride) {
+        const u32x4 qa = reinterpret_cast<const u32x4*>(earlier)[i];
+        const u32x4 qb = reinterpret_cast<const u32x4*>(current)[i];
+        T a[C], b[C], o[C];
+        __builtin_memcpy(a, &qa, 16);
+        __builtin_memcpy(b, &qb, 16);
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            o[k] = reduce2<T, M>(a[k], b[k]);
+        }
+        store_vec<T, C>(out + i * C, o);
+    }
+    for (uint64_t i = nvec * C + tid; i < n; i += stride) {
+        out[i] = reduce2<T, M>(earlier[i], current[i]);
+    }
+}
+
+// ---- dispatch ---------------------------------------------------------------
+
+template<typename F>
+hipError_t
+with_dtype(int dtype, F&& f)
+{
+    switch (dtype) {
+        case 0:
+            return f(uint8_t{});
+        case 1:
+            return f(uint16_t{});
+        case 2:
+            return f(uint32_t{});
+        case 3:
+            return f(uint64_t{});
+        case 4:
+            return f(int8_t{});
+        case 5:
+            return f(int16_t{});
+        case 6:
+            return f(int32_t{});
+        case 7:
+            return f(int64_t{});
+        case 8:
+            return f(float{});
+        case 9:
+            return f(double{});
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+template<typename F>
+hipError_t
+with_method(int method, F&& f)
+{
+    switch (method) {
+        case kDecimate:
+            return f(std::integral_constant<int, kDecimate>{});
+        case kMean:
+            return f(std::integral_constant<int, kMean>{});
+        case kMin:
+            return f(std::integral_constant<int, kMin>{});
+        case kMax:
+            return f(std::integral_constant<int, kMax>{});
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+uint32_t g_cascade_grid_cap = 0;
+
+uint32_t
+grid_for(uint64_t work_items, uint32_t per_block, uint32_t cap)
+{
+    uint64_t blocks = (work_items + per_block - 1) / per_block;
+    if (blocks < 1)
+        blocks = 1;
+    if (cap && blocks > cap)
+        blocks = cap;
+    return uint32_t(blocks);
+}
+
+} // namespace
+
+size_t
+dtype_bytes(int dtype)
+{
+    switch (dtype) {
+        case 0:
+        case 4:
+            return 1;
+        case 1:
+        case 5:
+            return 2;
+        case 2:
+        case 6:
+        case 8:
+            return 4;
+        case 3:
+        case 7:
+        case 9:
+            return 8;
+        default:
+            return 0;
+    }
+}
+
+bool
+dtype_valid(int dtype)
+{
+    return dtype_bytes(dtype) != 0;
+}
+
+bool
+method_valid(int method)
+{
+    return method >= kDecimate && method <= kMax;
+}
+
+void
+set_cascade_grid_cap(uint32_t blocks)
+{
+    g_cascade_grid_cap = blocks;
+}
+
+bool
+cascade_supported(int dtype,
+                  const void* src,
+                  uint32_t W,
+                  uint32_t H,
+                  const LevelOut* outs,
+                  int n_out)
+{
+    const size_t b = dtype_bytes(dtype);
+    if (!b || n_out < 1 || n_out > kMaxFusedLevels || W == 0 || H == 0)
+        return false;
+    const uint32_t C = uint32_t(16 / b);
+    if (W % C != 0)
+        return false;
+    if (reinterpret_cast<uintptr_t>(src) % 16 != 0)
+        return false;
+    uint32_t w = W, h = H;
+    for (int i = 0; i < n_out; ++i) {
+        w = (w + 1) / 2;
+        h = (h + 1) / 2;
+        if (outs[i].w != w || outs[i].h != h)
+            return false;
+        if (reinterpret_cast<uintptr_t>(outs[i].ptr) % 16 != 0)
+            return false;
+        if ((outs[i].frame_elems * b) % 16 != 0)
+            return false;
+    }
+    return true;
+}
+
+hipError_t
+launch_cascade(int dtype,
+               int method,
+               const void* src,
+               uint64_t src_frame_elems,
+               uint32_t W,
+               uint32_t H,
+               const LevelOut* outs,
+               int n_out,
+               uint32_t n_frames,
+               hipStream_t stream)
+{
+    if (!cascade_supported(dtype, src, W, H, outs, n_out) || n_frames == 0)
+        return hipErrorInvalidValue;
+    if ((src_frame_elems * dtype_bytes(dtype)) % 16 != 0)
+        return hipErrorInvalidValue;
+
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        constexpr uint32_t C = 16 / sizeof(T);
+        CascadeParams p{};
+        p.src = static_cast<const uint8_t*>(src);
+        p.src_frame_elems = src_frame_elems;
+        p.W = W;
+        p.H = H;
+        p.units_x = (W + 64 * C - 1) / (64 * C);
+        const uint32_t R = 1u << n_out;
+        p.units_y = (H + R - 1) / R;
+        const uint64_t total = uint64_t(p.units_x) * p.units_y * n_frames;
+        if (total >= (1ull << 31))
+            return hipErrorInvalidValue;
+        p.total_units = uint32_t(total);
+        for (int i = 0; i < n_out; ++i) {
+            p.dst[i] = static_cast<uint8_t*>(outs[i].ptr);
+            p.dst_frame_elems[i] = outs[i].frame_elems;
+            p.w[i] = outs[i].w;
+            p.h[i] = outs[i].h;
+        }
+        // 4 waves per block, one tile per wave per iteration.
+        const uint32_t grid = grid_for(total, 4, g_cascade_grid_cap);
+        return with_method(method, [&](auto mtag) -> hipError_t {
+            constexpr int M = decltype(mtag)::value;
+            switch (n_out) {
+                case 1:
+                    hipLaunchKernelGGL((cascade_kernel<T, M, 1>),
+                                       dim3(grid), dim3(256), 0, stream, p);
+                    break;
+                case 2:
+                    hipLaunchKernelGGL((cascade_kernel<T, M, 2>),
+                                       dim3(grid), dim3(256), 0, stream, p);
+                    break;
+                case 3:
+                    hipLaunchKernelGGL((cascade_kernel<T, M, 3>),
+                                       dim3(grid), dim3(256), 0, stream, p);
+                    break;
+                default:
+                    hipLaunchKernelGGL((cascade_kernel<T, M, 4>),
+                                       dim3(grid), dim3(256), 0, stream, p);
+                    break;
+            }
+            return hipGetLastError();
+        });
+    });
+}
+
+hipError_t
+launch_xy_generic(int dtype,
+                  int method,
+                  const void* src,
+                  uint64_t src_frame_elems,
+                  uint32_t w,
+                  uint32_t h,
+                  const LevelOut& out,
+                  uint32_t n_frames,
+                  hipStream_t stream)
+{
+    if (w == 0 || h == 0 || n_frames == 0)
+        return hipErrorInvalidValue;
+    if (out.w != (w + 1) / 2 || out.h != (h + 1) / 2)
+        return hipErrorInvalidValue;
+    const uint64_t total = uint64_t(out.w) * out.h * n_frames;
+    const uint32_t grid = grid_for(total, 256, 8192);
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        return with_method(method, [&](auto mtag) -> hipError_t {
+            constexpr int M = decltype(mtag)::value;
+            hipLaunchKernelGGL((xy_generic_kernel<T, M>),
+                               dim3(grid), dim3(256), 0, stream,
+                               static_cast<const T*>(src), src_frame_elems, w,
+                               h, static_cast<T*>(out.ptr), out.frame_elems,
+                               out.w, out.h, total);
+            return hipGetLastError();
+        });
+    });
+}
+
+hipError_t
+launch_zpair(int dtype,
+             int method,
+             void* out,
+             const void* earlier,
+             const void* current,
+             uint64_t n,
+             hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(out) |
+                        reinterpret_cast<uintptr_t>(earlier) |
+                        reinterpret_cast<uintptr_t>(current);
+    if (a % 16 != 0)
+        return hipErrorInvalidValue;
+    const size_t b = dtype_bytes(dtype);
+    if (!b)
+        return hipErrorInvalidValue;
+    const uint64_t nvec = (n * b + 15) / 16;
+    const uint32_t grid = grid_for(nvec, 256, 8192);
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        return with_method(method, [&](auto mtag) -> hipError_t {
+            constexpr int M = decltype(mtag)::value;
+            hipLaunchKernelGGL((zpair_kernel<T, M>), dim3(grid), dim3(256), 0,
+                               stream, static_cast<T*>(out),
+                               static_cast<const T*>(earlier),
+                               static_cast<const T*>(current), n);
+            return hipGetLastError();
+        });
+    });
+}
+
+} // namespace aqz

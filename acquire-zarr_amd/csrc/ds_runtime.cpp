@@ -1,0 +1,749 @@
+// ds_runtime.cpp — implementation of the C ABI in include/aqz_downsampler.h.
+//
+// Host orchestration of the per-frame pyramid on one MI355X:
+//   * the level planner (restates downsampler.cpp:8-37, 493-597);
+//   * the add_frame state machine (restates downsampler.cpp:306-401): level
+//     cascade, Z pairing against the stored earlier plane, odd-plane
+//     pass-through, emit-without-overwrite (:599-605);
+//   * take_frame (:403-414) served from pinned host buffers filled by async
+//     device->host copies queued behind the kernels.
+// Runs of consecutive levels that only halve XY are fused into one cascade
+// launch (up to 4 levels per launch), so the frame is read from HBM once.
+#include "aqz_downsampler.h"
+#include "ds_kernels.hh"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void
+set_global_error(const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+uint32_t
+bit_width(uint32_t x)
+{
+    uint32_t n = 0;
+    for (; x; x >>= 1)
+        ++n;
+    return n;
+}
+
+// Number of 2x divisions a dimension supports before it fits one chunk
+// (downsampler.cpp:507-520): bit_width(ceil(size/chunk) - 1).
+uint32_t
+divisions(const aqz_dimension& d)
+{
+    const uint32_t n = (d.array_size_px + d.chunk_size_px - 1) / d.chunk_size_px;
+    return n > 1 ? bit_width(n - 1) : 0;
+}
+
+// downsample_dimension, downsampler.cpp:8-37.
+aqz_dimension
+halve(const aqz_dimension& d)
+{
+    aqz_dimension o = d;
+    o.array_size_px = (d.array_size_px + d.array_size_px % 2) / 2;
+    const uint32_t n = (o.array_size_px + d.chunk_size_px - 1) / d.chunk_size_px;
+    o.shard_size_chunks = std::min(n, d.shard_size_chunks);
+    o.scale = d.scale * 2.0;
+    return o;
+}
+
+} // namespace
+
+struct aqz_ds
+{
+    int device = 0;
+    int dtype = 0;
+    int method = 0;
+    size_t bpp = 0;
+    uint32_t n = 0;
+    std::vector<aqz_level_desc> lv;
+    std::vector<size_t> bytes;      // bytes of one frame per level
+    std::vector<uint8_t> xy;        // level L halves XY (L >= 1)
+    std::vector<uint8_t> zh;        // level L halves Z (L >= 1)
+    std::vector<uint32_t> count;    // level_frame_count_
+    std::vector<uint8_t> has_partial;
+
+    hipStream_t stream = nullptr;
+    void* d_in = nullptr;           // level-0 staging on device
+    std::vector<void*> d_level;     // level output buffers
+    std::vector<void*> d_partial;   // stored earlier plane (Z levels)
+    void* h_stage = nullptr;        // pinned level-0 staging
+    hipEvent_t stage_done = nullptr;
+    std::vector<void*> h_level;     // pinned take_frame cache
+    std::vector<uint8_t> cached;
+    std::vector<hipEvent_t> ready;
+    size_t device_bytes = 0;
+
+    std::string err;
+
+    int fail(hipError_t e, const char* what)
+    {
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return AQZ_INTERNAL_ERROR;
+    }
+    int fail_arg(const std::string& what)
+    {
+        err = what;
+        return AQZ_INVALID_ARGUMENT;
+    }
+};
+
+namespace {
+
+#define HIP_TRY(ds, expr, what)                                                \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess)                                                  \
+            return (ds)->fail(e_, what);                                       \
+    } while (0)
+
+// Where the frames a level emits go.
+struct Sink
+{
+    // cache mode (add_frame): async D2H into the pinned take_frame slot
+    bool batch = false;
+    // batch mode: frame k of level L goes to out[L] + k*bytes[L]
+    void* const* out = nullptr;
+    std::vector<uint32_t>* emitted = nullptr;
+};
+
+uint64_t
+elems(const aqz_ds* ds, uint32_t level)
+{
+    return uint64_t(ds->lv[level].width) * ds->lv[level].height;
+}
+
+// emplace_downsampled_frame_ (downsampler.cpp:599-605).
+int
+emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink)
+{
+    ++ds->count[level];
+    if (sink.batch) {
+        auto& k = (*sink.emitted)[level];
+        uint8_t* dst = static_cast<uint8_t*>(sink.out[level]) + k * ds->bytes[level];
+        ++k;
+        if (dst != d_frame) {
+            HIP_TRY(ds,
+                    hipMemcpyAsync(dst, d_frame, ds->bytes[level],
+                                   hipMemcpyDeviceToDevice, ds->stream),
+                    "hipMemcpyAsync D2D");
+        }
+        return AQZ_OK;
+    }
+    // unordered_map::emplace keeps an untaken frame; the new one is dropped.
+    if (ds->cached[level])
+        return AQZ_OK;
+    HIP_TRY(ds,
+            hipMemcpyAsync(ds->h_level[level], d_frame, ds->bytes[level],
+                           hipMemcpyDeviceToHost, ds->stream),
+            "hipMemcpyAsync D2H");
+    HIP_TRY(ds, hipEventRecord(ds->ready[level], ds->stream), "hipEventRecord");
+    ds->cached[level] = 1;
+    return AQZ_OK;
+}
+
+// XY-reduce `src` (level L-1 geometry) into `dst` (level L geometry).
+int
+reduce_xy(aqz_ds* ds, uint32_t L, const void* src, void* dst)
+{
+    const aqz_level_desc& a = ds->lv[L - 1];
+    aqz::LevelOut o{ dst, elems(ds, L), ds->lv[L].width, ds->lv[L].height };
+    hipError_t e;
+    if (aqz::cascade_supported(ds->dtype, src, a.width, a.height, &o, 1))
+        e = aqz::launch_cascade(ds->dtype, ds->method, src, elems(ds, L - 1),
+                                a.width, a.height, &o, 1, 1, ds->stream);
+    else
+        e = aqz::launch_xy_generic(ds->dtype, ds->method, src, elems(ds, L - 1),
+                                   a.width, a.height, o, 1, ds->stream);
+    HIP_TRY(ds, e, "xy level kernel");
+    return AQZ_OK;
+}
+
+// One frame through the level cascade: Downsampler::add_frame
+// (downsampler.cpp:306-401) with device buffers.
+int
+process_frame(aqz_ds* ds, const void* d_frame, const Sink& sink)
+{
+    ++ds->count[0];
+    const void* cur = d_frame;
+    uint32_t L = 1;
+    while (L < ds->n) {
+        if (ds->xy[L] && !ds->zh[L]) {
+            // Run of pure-XY levels: they always emit, fuse up to 4.
+            uint32_t k = 1;
+            while (L + k < ds->n && k < aqz::kMaxFusedLevels && ds->xy[L + k] &&
+                   !ds->zh[L + k])
+                ++k;
+            aqz::LevelOut outs[aqz::kMaxFusedLevels];
+            for (uint32_t j = 0; j < k; ++j) {
+                void* dst = ds->d_level[L + j];
+                if (sink.batch) {
+                    // write straight into the caller's batch slot
+                    dst = static_cast<uint8_t*>(sink.out[L + j]) +
+                          (*sink.emitted)[L + j] * ds->bytes[L + j];
+                }
+                outs[j] = { dst, elems(ds, L + j), ds->lv[L + j].width,
+                            ds->lv[L + j].height };
+            }
+            const aqz_level_desc& a = ds->lv[L - 1];
+            if (aqz::cascade_supported(ds->dtype, cur, a.width, a.height, outs,
+                                       int(k))) {
+                HIP_TRY(ds,
+                        aqz::launch_cascade(ds->dtype, ds->method, cur,
+                                            elems(ds, L - 1), a.width, a.height,
+                                            outs, int(k), 1, ds->stream),
+                        "cascade kernel");
+            } else {
+                const void* s = cur;
+                for (uint32_t j = 0; j < k; ++j) {
+                    const aqz_level_desc& b = ds->lv[L + j - 1];
+                    HIP_TRY(ds,
+                            aqz::launch_xy_generic(ds->dtype, ds->method, s,
+                                                   elems(ds, L + j - 1), b.width,
+                                                   b.height, outs[j], 1,
+                                                   ds->stream),
+                            "xy level kernel");
+                    s = outs[j].ptr;
+                }
+            }
+            for (uint32_t j = 0; j < k; ++j) {
+                int rc = emit(ds, L + j, outs[j].ptr, sink);
+                if (rc)
+                    return rc;
+            }
+            cur = outs[k - 1].ptr;
+            L += k;
+            continue;
+        }
+
+        // General level: optional XY reduce, then optional Z pairing.
+        const uint32_t prev_planes = ds->lv[L - 1].planes;
+        bool average = ds->zh[L] != 0;
+        if (prev_planes % 2 != 0 && ds->count[L - 1] % prev_planes == 0)
+            average = false; // last plane of an odd stack passes through
+
+        if (average && !ds->has_partial[L]) {
+            // store this plane as the earlier half of the pair, then stop
+            if (ds->xy[L]) {
+                int rc = reduce_xy(ds, L, cur, ds->d_partial[L]);
+                if (rc)
+                    return rc;
+            } else {
+                HIP_TRY(ds,
+                        hipMemcpyAsync(ds->d_partial[L], cur, ds->bytes[L],
+                                       hipMemcpyDeviceToDevice, ds->stream),
+                        "hipMemcpyAsync D2D");
+            }
+            ds->has_partial[L] = 1;
+            break;
+        }
+
+        const void* next = cur;
+        if (ds->xy[L]) {
+            int rc = reduce_xy(ds, L, cur, ds->d_level[L]);
+            if (rc)
+                return rc;
+            next = ds->d_level[L];
+        }
+        if (average) {
+            // average_two_frames(dst = earlier, src = current)
+            HIP_TRY(ds,
+                    aqz::launch_zpair(ds->dtype, ds->method, ds->d_level[L],
+                                      ds->d_partial[L], next, elems(ds, L),
+                                      ds->stream),
+                    "zpair kernel");
+            ds->has_partial[L] = 0;
+            next = ds->d_level[L];
+        }
+        int rc = emit(ds, L, next, sink);
+        if (rc)
+            return rc;
+        cur = next;
+        ++L;
+    }
+    return AQZ_OK;
+}
+
+int
+bind_device(aqz_ds* ds)
+{
+    HIP_TRY(ds, hipSetDevice(ds->device), "hipSetDevice");
+    return AQZ_OK;
+}
+
+void
+release(aqz_ds* ds)
+{
+    if (!ds)
+        return;
+    // Best-effort teardown: errors here have nowhere to go.
+    (void)hipSetDevice(ds->device);
+    if (ds->stream)
+        (void)hipStreamSynchronize(ds->stream);
+    (void)hipFree(ds->d_in);
+    for (void* p : ds->d_level)
+        (void)hipFree(p);
+    for (void* p : ds->d_partial)
+        (void)hipFree(p);
+    (void)hipHostFree(ds->h_stage);
+    for (void* p : ds->h_level)
+        (void)hipHostFree(p);
+    for (hipEvent_t e : ds->ready)
+        if (e)
+            (void)hipEventDestroy(e);
+    if (ds->stage_done)
+        (void)hipEventDestroy(ds->stage_done);
+    if (ds->stream)
+        (void)hipStreamDestroy(ds->stream);
+    delete ds;
+}
+
+} // namespace
+
+extern "C" {
+
+int
+aqz_plan_levels(const aqz_dimension* dims,
+                uint32_t ndims,
+                uint32_t max_levels,
+                aqz_dimension* out,
+                uint32_t out_cap_levels,
+                uint32_t* n_levels)
+{
+    if (!dims || !n_levels || ndims < 3 || ndims > AQZ_MAX_DIMS) {
+        set_global_error("plan_levels: need 3..%d dimensions", AQZ_MAX_DIMS);
+        return AQZ_INVALID_ARGUMENT;
+    }
+    for (uint32_t i = 0; i < ndims; ++i) {
+        if (dims[i].chunk_size_px == 0) {
+            set_global_error("plan_levels: dimension %u has chunk size 0", i);
+            return AQZ_INVALID_ARGUMENT;
+        }
+    }
+    const aqz_dimension& x = dims[ndims - 1];
+    const aqz_dimension& y = dims[ndims - 2];
+    const aqz_dimension& z = dims[ndims - 3];
+    uint32_t levels = std::min(divisions(x), divisions(y));
+    if (z.type == AQZ_DIM_SPACE)
+        levels = std::max(levels, divisions(z));
+    if (max_levels > 0)
+        levels = std::min(levels, max_levels);
+    *n_levels = levels + 1;
+    if (!out)
+        return AQZ_OK;
+    if (out_cap_levels < levels + 1) {
+        set_global_error("plan_levels: room for %u levels, need %u",
+                         out_cap_levels, levels + 1);
+        return AQZ_OVERFLOW;
+    }
+    std::copy(dims, dims + ndims, out);
+    for (uint32_t l = 1; l <= levels; ++l) {
+        const aqz_dimension* p = out + size_t(l - 1) * ndims;
+        aqz_dimension* c = out + size_t(l) * ndims;
+        std::copy(p, p + ndims - 3, c);
+        const aqz_dimension& pz = p[ndims - 3];
+        c[ndims - 3] = (pz.type == AQZ_DIM_SPACE && pz.array_size_px > pz.chunk_size_px)
+                         ? halve(pz)
+                         : pz;
+        const aqz_dimension& py = p[ndims - 2];
+        const aqz_dimension& px = p[ndims - 1];
+        const bool shrink_xy = std::min(py.array_size_px, px.array_size_px) >
+                               std::max(py.chunk_size_px, px.chunk_size_px);
+        c[ndims - 2] = shrink_xy ? halve(py) : py;
+        c[ndims - 1] = shrink_xy ? halve(px) : px;
+    }
+    return AQZ_OK;
+}
+
+int
+aqz_ds_create(const aqz_level_desc* levels,
+              uint32_t n_levels,
+              int dtype,
+              int method,
+              int device,
+              aqz_ds** out)
+{
+    if (!out) {
+        set_global_error("create: null output handle");
+        return AQZ_INVALID_ARGUMENT;
+    }
+    *out = nullptr;
+    if (!levels || n_levels == 0 || n_levels > AQZ_MAX_LEVELS) {
+        set_global_error("create: need 1..%d levels", AQZ_MAX_LEVELS);
+        return AQZ_INVALID_ARGUMENT;
+    }
+    if (!aqz::dtype_valid(dtype)) {
+        set_global_error("Invalid data type: %d", dtype);
+        return AQZ_INVALID_ARGUMENT;
+    }
+    if (!aqz::method_valid(method)) {
+        set_global_error("Invalid downsampling method: %d", method);
+        return AQZ_INVALID_ARGUMENT;
+    }
+    for (uint32_t l = 0; l < n_levels; ++l) {
+        if (levels[l].width == 0 || levels[l].height == 0) {
+            set_global_error("create: level %u has an empty frame", l);
+            return AQZ_INVALID_ARGUMENT;
+        }
+        if (l > 0) {
+            const aqz_level_desc& a = levels[l - 1];
+            const aqz_level_desc& b = levels[l];
+            const bool same = b.width == a.width && b.height == a.height;
+            const bool half = b.width == (a.width + 1) / 2 &&
+                              b.height == (a.height + 1) / 2;
+            // scale_image always halves both; anything else fails the
+            // reference's dimension EXPECTs (downsampler.cpp:348-356).
+            if (!same && !half) {
+                set_global_error("create: level %u is neither a copy nor a 2x "
+                                 "reduction of level %u", l, l - 1);
+                return AQZ_INVALID_ARGUMENT;
+            }
+        }
+    }
+
+    if (device < 0) {
+        const char* env = std::getenv("AQZ_GPU_DEVICE");
+        if (env && *env) {
+            device = std::atoi(env);
+        } else if (hipGetDevice(&device) != hipSuccess) {
+            device = 0;
+        }
+    }
+
+    auto* ds = new aqz_ds();
+    ds->device = device;
+    ds->dtype = dtype;
+    ds->method = method;
+    ds->bpp = aqz::dtype_bytes(dtype);
+    ds->n = n_levels;
+    ds->lv.assign(levels, levels + n_levels);
+    ds->bytes.resize(n_levels);
+    ds->xy.assign(n_levels, 0);
+    ds->zh.assign(n_levels, 0);
+    ds->count.assign(n_levels, 0);
+    ds->has_partial.assign(n_levels, 0);
+    ds->d_level.assign(n_levels, nullptr);
+    ds->d_partial.assign(n_levels, nullptr);
+    ds->h_level.assign(n_levels, nullptr);
+    ds->cached.assign(n_levels, 0);
+    ds->ready.assign(n_levels, nullptr);
+    for (uint32_t l = 0; l < n_levels; ++l) {
+        ds->bytes[l] = size_t(levels[l].width) * levels[l].height * ds->bpp;
+        if (l > 0) {
+            ds->xy[l] = levels[l].width < levels[l - 1].width ||
+                        levels[l].height < levels[l - 1].height;
+            ds->zh[l] = levels[l].planes < levels[l - 1].planes;
+        }
+    }
+
+    auto fail = [&](hipError_t e, const char* what) {
+        const int code = e == hipErrorOutOfMemory ? AQZ_OUT_OF_MEMORY
+                                                  : AQZ_INTERNAL_ERROR;
+        set_global_error("%s: %s", what, hipGetErrorString(e));
+        release(ds);
+        return code;
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess)
+        return fail(e, "hipSetDevice");
+    if ((e = hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(e, "hipStreamCreate");
+    if ((e = hipEventCreateWithFlags(&ds->stage_done, hipEventDisableTiming)) != hipSuccess)
+        return fail(e, "hipEventCreate");
+    if ((e = hipMalloc(&ds->d_in, ds->bytes[0])) != hipSuccess)
+        return fail(e, "hipMalloc level 0");
+    if ((e = hipHostMalloc(&ds->h_stage, ds->bytes[0], hipHostMallocDefault)) != hipSuccess)
+        return fail(e, "hipHostMalloc staging");
+    ds->device_bytes = ds->bytes[0];
+    for (uint32_t l = 1; l < n_levels; ++l) {
+        if ((e = hipMalloc(&ds->d_level[l], ds->bytes[l])) != hipSuccess)
+            return fail(e, "hipMalloc level");
+        ds->device_bytes += ds->bytes[l];
+        if (ds->zh[l]) {
+            if ((e = hipMalloc(&ds->d_partial[l], ds->bytes[l])) != hipSuccess)
+                return fail(e, "hipMalloc partial");
+            ds->device_bytes += ds->bytes[l];
+        }
+        if ((e = hipHostMalloc(&ds->h_level[l], ds->bytes[l], hipHostMallocDefault)) != hipSuccess)
+            return fail(e, "hipHostMalloc level");
+        if ((e = hipEventCreateWithFlags(&ds->ready[l], hipEventDisableTiming)) != hipSuccess)
+            return fail(e, "hipEventCreate");
+    }
+    *out = ds;
+    return AQZ_OK;
+}
+
+void
+aqz_ds_destroy(aqz_ds* ds)
+{
+    release(ds);
+}
+
+int
+aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (!host_frame || nbytes != ds->bytes[0])
+        return ds->fail_arg("add_frame: expected " + std::to_string(ds->bytes[0]) +
+                            " bytes, got " + std::to_string(nbytes));
+    if (int rc = bind_device(ds))
+        return rc;
+    // The staging buffer is free once the previous frame's upload finished.
+    HIP_TRY(ds, hipEventSynchronize(ds->stage_done), "hipEventSynchronize");
+    std::memcpy(ds->h_stage, host_frame, nbytes);
+    HIP_TRY(ds,
+            hipMemcpyAsync(ds->d_in, ds->h_stage, nbytes, hipMemcpyHostToDevice,
+                           ds->stream),
+            "hipMemcpyAsync H2D");
+    HIP_TRY(ds, hipEventRecord(ds->stage_done, ds->stream), "hipEventRecord");
+    return process_frame(ds, ds->d_in, Sink{});
+}
+
+int
+aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (!device_frame || nbytes != ds->bytes[0])
+        return ds->fail_arg("add_device_frame: expected " +
+                            std::to_string(ds->bytes[0]) + " bytes, got " +
+                            std::to_string(nbytes));
+    if (int rc = bind_device(ds))
+        return rc;
+    return process_frame(ds, device_frame, Sink{});
+}
+
+int
+aqz_ds_take_frame(aqz_ds* ds,
+                  uint32_t level,
+                  void* dst,
+                  size_t cap,
+                  size_t* nbytes,
+                  int* has_frame)
+{
+    if (!ds || !has_frame)
+        return AQZ_INVALID_ARGUMENT;
+    *has_frame = 0;
+    if (level == 0 || level >= ds->n)
+        return AQZ_OK; // the reference's map lookup simply misses
+    if (!ds->cached[level])
+        return AQZ_OK;
+    *has_frame = 1;
+    if (nbytes)
+        *nbytes = ds->bytes[level];
+    if (!dst)
+        return AQZ_OK;
+    if (cap < ds->bytes[level])
+        return ds->fail_arg("take_frame: buffer too small");
+    if (int rc = bind_device(ds))
+        return rc;
+    HIP_TRY(ds, hipEventSynchronize(ds->ready[level]), "hipEventSynchronize");
+    std::memcpy(dst, ds->h_level[level], ds->bytes[level]);
+    ds->cached[level] = 0;
+    return AQZ_OK;
+}
+
+int
+aqz_ds_run_device_batch(aqz_ds* ds,
+                        const void* device_frames,
+                        uint32_t n_frames,
+                        void* const* device_out_levels,
+                        uint32_t* out_counts,
+                        void* hip_stream)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (!device_frames || !device_out_levels)
+        return ds->fail_arg("run_device_batch: null buffer");
+    for (uint32_t l = 1; l < ds->n; ++l)
+        if (!device_out_levels[l])
+            return ds->fail_arg("run_device_batch: null output for level " +
+                                std::to_string(l));
+    if (int rc = bind_device(ds))
+        return rc;
+    hipStream_t user = static_cast<hipStream_t>(hip_stream);
+    hipStream_t saved = ds->stream;
+    if (user)
+        ds->stream = user;
+
+    std::vector<uint32_t> emitted(ds->n, 0);
+    int rc = AQZ_OK;
+
+    bool pure_xy = ds->n > 1;
+    for (uint32_t l = 1; l < ds->n; ++l)
+        pure_xy = pure_xy && ds->xy[l] && !ds->zh[l];
+
+    aqz::LevelOut outs[aqz::kMaxFusedLevels];
+    const uint32_t k0 = std::min<uint32_t>(ds->n - 1, aqz::kMaxFusedLevels);
+    for (uint32_t j = 0; pure_xy && j < k0; ++j)
+        outs[j] = { device_out_levels[1 + j], elems(ds, 1 + j),
+                    ds->lv[1 + j].width, ds->lv[1 + j].height };
+
+    if (pure_xy && n_frames > 0 &&
+        aqz::cascade_supported(ds->dtype, device_frames, ds->lv[0].width,
+                               ds->lv[0].height, outs, int(k0))) {
+        // Whole batch, every frame independent: one launch per 4 levels.
+        uint32_t L = 1;
+        const void* src = device_frames;
+        while (L < ds->n && rc == AQZ_OK) {
+            const uint32_t k = std::min<uint32_t>(ds->n - L, aqz::kMaxFusedLevels);
+            for (uint32_t j = 0; j < k; ++j)
+                outs[j] = { device_out_levels[L + j], elems(ds, L + j),
+                            ds->lv[L + j].width, ds->lv[L + j].height };
+            const aqz_level_desc& a = ds->lv[L - 1];
+            hipError_t e;
+            if (aqz::cascade_supported(ds->dtype, src, a.width, a.height, outs,
+                                       int(k))) {
+                e = aqz::launch_cascade(ds->dtype, ds->method, src,
+                                        elems(ds, L - 1), a.width, a.height,
+                                        outs, int(k), n_frames, ds->stream);
+            } else {
+                e = hipSuccess;
+                const void* s = src;
+                for (uint32_t j = 0; j < k && e == hipSuccess; ++j) {
+                    const aqz_level_desc& b = ds->lv[L + j - 1];
+                    e = aqz::launch_xy_generic(ds->dtype, ds->method, s,
+                                               elems(ds, L + j - 1), b.width,
+                                               b.height, outs[j], n_frames,
+                                               ds->stream);
+                    s = outs[j].ptr;
+                }
+            }
+            if (e != hipSuccess)
+                rc = ds->fail(e, "batch cascade");
+            src = outs[k - 1].ptr;
+            L += k;
+        }
+        for (uint32_t l = 0; l < ds->n; ++l) {
+            ds->count[l] += n_frames;
+            emitted[l] = n_frames;
+        }
+    } else {
+        Sink sink;
+        sink.batch = true;
+        sink.out = device_out_levels;
+        sink.emitted = &emitted;
+        const uint8_t* base = static_cast<const uint8_t*>(device_frames);
+        for (uint32_t i = 0; i < n_frames && rc == AQZ_OK; ++i)
+            rc = process_frame(ds, base + size_t(i) * ds->bytes[0], sink);
+        emitted[0] = n_frames;
+    }
+    if (out_counts)
+        std::copy(emitted.begin(), emitted.end(), out_counts);
+    ds->stream = saved;
+    return rc;
+}
+
+size_t
+aqz_ds_level_bytes(const aqz_ds* ds, uint32_t level)
+{
+    return (ds && level < ds->n) ? ds->bytes[level] : 0;
+}
+
+uint32_t
+aqz_ds_level_count(const aqz_ds* ds)
+{
+    return ds ? ds->n : 0;
+}
+
+size_t
+aqz_ds_device_memory_usage(const aqz_ds* ds)
+{
+    return ds ? ds->device_bytes : 0;
+}
+
+const char*
+aqz_ds_last_error(const aqz_ds* ds)
+{
+    return ds ? ds->err.c_str() : "null handle";
+}
+
+const char*
+aqz_last_error(void)
+{
+    return g_last_error.c_str();
+}
+
+const char*
+aqz_method_name(int method)
+{
+    // Downsampler::downsampling_method, downsampler.cpp:422-437
+    switch (method) {
+        case AQZ_METHOD_DECIMATE:
+            return "decimate";
+        case AQZ_METHOD_MEAN:
+            return "local_mean";
+        case AQZ_METHOD_MIN:
+            return "local_min";
+        case AQZ_METHOD_MAX:
+            return "local_max";
+        default:
+            return nullptr;
+    }
+}
+
+const char*
+aqz_method_metadata_json(int method)
+{
+    // Downsampler::get_metadata, downsampler.cpp:440-485: the OME
+    // `multiscales[0].metadata` object (nlohmann::json serialises keys in
+    // sorted order).
+    switch (method) {
+        case AQZ_METHOD_MEAN:
+            return "{\"description\":\"The fields in the metadata describe how "
+                   "to reproduce this multiscaling in scikit-image. The method "
+                   "and its parameters are given here.\",\"kwargs\":{\"cval\":"
+                   "\"0\",\"factors\":\"(2, 2)\"},\"method\":\"skimage."
+                   "transform.downscale_local_mean\",\"version\":\"0.25.2\"}";
+        case AQZ_METHOD_DECIMATE:
+            return "{\"args\":[\"(slice(0, None, 2), slice(0, None, 2))\"],"
+                   "\"description\":\"Subsampling by taking every 2nd "
+                   "pixel/voxel (top-left corner of each 2x2 block). "
+                   "Equivalent to numpy array slicing with stride 2.\","
+                   "\"method\":\"np.ndarray.__getitem__\",\"version\":"
+                   "\"2.2.6\"}";
+        case AQZ_METHOD_MIN:
+            return "{\"description\":\"Minimum pooling over 2x2 blocks. "
+                   "Equivalent to reshaping into blocks and taking numpy.min "
+                   "along block dimensions.\",\"kwargs\":{\"func\":\"np.min\"},"
+                   "\"method\":\"skimage.measure.block_reduce\",\"version\":"
+                   "\"0.25.2\"}";
+        case AQZ_METHOD_MAX:
+            return "{\"description\":\"Maximum pooling over 2x2 blocks. "
+                   "Equivalent to reshaping into blocks and taking numpy.max "
+                   "along block dimensions.\",\"kwargs\":{\"func\":\"np.max\"},"
+                   "\"method\":\"skimage.measure.block_reduce\",\"version\":"
+                   "\"0.25.2\"}";
+        default:
+            return nullptr;
+    }
+}
+
+const char*
+aqz_version(void)
+{
+    return "aqz-mi355x 0.1.0 (gfx950)";
+}
+
+} // extern "C"

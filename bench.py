@@ -1,0 +1,250 @@
+"""bench.py — device-resident multiscale downsample throughput on MI355X.
+
+Metric (BASELINE.json): GPixels/s device-resident multiscale downsample,
+4096^2 uint16, 5 levels.  GPix/s counts base-level pixels
+(frames x W x H / time).  One "step" = one pass of the hot path over one
+batch of B frames already resident in HBM on every rank: the whole pyramid
+(levels 1..4) of every frame, written to HBM.  It is one fused cascade
+launch per step (aqz_ds_run_device_batch).
+
+Multi-GPU: one process per GPU (torchrun); frames are independent, so each
+rank runs its own batch with no data-path collective (weak scaling); the
+barrier and the max-over-ranks of the timed region use torch.distributed.
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+`roofline` (algorithmic bytes / average kernel duration from HIP events on the
+launch stream, against the 8 TB/s HBM peak), `cpu_baseline` (the C oracle —
+a single-thread port of the reference algorithm — on a bounded sample on this
+host), and `e2e` (host frame -> pinned H2D -> kernels -> D2H -> take_frame
+through the streaming API, the path's real end-to-end rate).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+WORKLOADS = {
+    # name: (width, height, dtype, chunk) — levels come from the planner
+    "4096x4096_u16": (4096, 4096, np.uint16, 256),   # headline, configs[2]
+    "2048x2048_u16": (2048, 2048, np.uint16, 256),   # configs[1]
+    "4096x4096_f32": (4096, 4096, np.float32, 256),  # configs[3] (per GPU)
+    "512x512_u8": (512, 512, np.uint8, 128),         # configs[0] synthetic
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="4096x4096_u16", choices=sorted(WORKLOADS))
+    p.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    p.add_argument("--method", default="mean", choices=["decimate", "mean", "min", "max"])
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--e2e-frames", type=int, default=48,
+                   help="frames through the streaming host API (0 disables)")
+    p.add_argument("--no-check", action="store_true",
+                   help="skip the one-frame oracle spot check")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch  # plumbing: device buffers, events, process group
+    import aqz_pkg
+    aqz = aqz_pkg.load()
+    aqz.lib()  # fail loudly if the native library is missing
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    W, H, dtype, chunk = WORKLOADS[args.workload]
+    method = aqz.METHODS[args.method]
+    dims = [(aqz.TIME, 0, 1, 1), (aqz.SPACE, H, chunk, 1), (aqz.SPACE, W, chunk, 1)]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    n_levels = len(geo)
+    bpp = np.dtype(dtype).itemsize
+    B = args.batch
+    frame_bytes = W * H * bpp
+
+    # synthetic input, resident in HBM before timing (seeded per rank)
+    gen = torch.Generator(device="cuda").manual_seed(0xA0C2A11 + rank)
+    if np.dtype(dtype).kind == "f":
+        d_in = (torch.rand(B * W * H, device="cuda", generator=gen) * 2000 - 1000
+                ).to(torch.float32).view(torch.uint8)
+    else:
+        d_in = torch.randint(0, 256, (B * frame_bytes,), dtype=torch.uint8,
+                             device="cuda", generator=gen)
+    outs = [None] + [torch.empty(B * w * h * bpp, dtype=torch.uint8, device="cuda")
+                     for w, h, _ in geo[1:]]
+    out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
+    ds = aqz.Downsampler(geo, dtype, method, device=local_rank)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    def step():
+        ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
+
+    # correctness spot check of one frame against the oracle (rank 0, N=1)
+    check = None
+    if not args.no_check and rank == 0:
+        import oracle as orc_mod  # test infrastructure: checker only
+        step()
+        torch.cuda.synchronize()
+        f0 = d_in[:frame_bytes].cpu().numpy().view(dtype).reshape(H, W)
+        ref = orc_mod.cascade_2d(f0, n_levels, method)
+        ok = True
+        for L in range(1, n_levels):
+            w, h, _ = geo[L]
+            got = outs[L][: w * h * bpp].cpu().numpy().view(dtype).reshape(h, w)
+            ok = ok and np.array_equal(got.view(np.uint8), ref[L - 1].view(np.uint8))
+        check = "bit-exact" if ok else "MISMATCH"
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-launch kernel timing with HIP events on the launch stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = [a.elapsed_time(b) for a, b in evs]
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    pixels = world * B * W * H * args.steps
+    value = pixels / elapsed / 1e9
+
+    alg_bytes = B * aqz.alg_bytes_per_frame(geo, bpp)  # per launch (one step)
+    avg_launch_s = float(np.mean(launch_ms)) / 1e3
+    achieved = alg_bytes / avg_launch_s / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                "min_launch_us": round(min(launch_ms) * 1e3, 2)}
+
+    cpu_baseline = None
+    e2e = None
+    if rank == 0 and world == 1:
+        if args.cpu_seconds > 0:
+            cpu_baseline = measure_cpu(dtype, W, H, n_levels, method, args.cpu_seconds,
+                                       d_in[:frame_bytes].cpu().numpy().view(dtype))
+        if args.e2e_frames > 0:
+            e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, local_rank)
+
+    if rank == 0:
+        line = {
+            "metric": "GPixels/s device-resident multiscale downsample, 4096² uint16, 5 levels",
+            "value": round(value, 2),
+            "unit": "GPixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": np.dtype(dtype).name.replace("uint", "u").replace("float", "f"),
+            "data": "synthetic (uniform random, seeded per rank)",
+            "config": {"workload": f"{W}x{H} {np.dtype(dtype).name}, {n_levels} levels, "
+                                   f"{args.method}, device-resident batch",
+                       "frames_per_step_per_gpu": B, "levels": n_levels,
+                       "parallelism": f"frame-sharded x{world}, no collective",
+                       "check": check},
+            "roofline": roofline,
+            "cpu_baseline": cpu_baseline,
+            "e2e": e2e,
+        }
+        print(json.dumps(line), flush=True)
+    ds.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def measure_cpu(dtype, W, H, n_levels, method, seconds, frame):
+    """The oracle (single-thread C port of the reference algorithm) on a
+    bounded sample of the same workload: whole frames until `seconds`."""
+    import oracle as orc_mod  # cpu_baseline leg: the only non-test user
+    frame = np.ascontiguousarray(frame.reshape(H, W))
+    orc_mod.cascade_2d(frame, n_levels, method)  # warm
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        orc_mod.cascade_2d(frame, n_levels, method)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    return {"value": round(n * W * H / el / 1e9, 4), "unit": "GPixels/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{n} frames of {W}x{H} {np.dtype(dtype).name}, {n_levels} levels, "
+                      f"{el:.1f} s, oracle/ds_oracle.c single thread (-O3 -mavx2)",
+            "ms_per_frame": round(el / n * 1e3, 2)}
+
+
+def measure_e2e(aqz, geo, dtype, method, n_frames, device):
+    """Streaming drop-in path: pageable host frame -> pinned staging -> H2D ->
+    fused kernels -> D2H of levels 1..N -> take_frame copies."""
+    W, H, _ = geo[0]
+    rng = np.random.default_rng(3)
+    if np.dtype(dtype).kind == "f":
+        frames = [rng.uniform(-1000, 1000, (H, W)).astype(dtype) for _ in range(4)]
+    else:
+        frames = [rng.integers(0, np.iinfo(dtype).max, (H, W), dtype=dtype,
+                               endpoint=True) for _ in range(4)]
+    ds = aqz.Downsampler(geo, dtype, method, device=device)
+    for i in range(3):
+        ds.add_frame(frames[i % 4])
+        for L in range(1, len(geo)):
+            ds.take_frame(L)
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        ds.add_frame(frames[i % 4])
+        for L in range(1, len(geo)):
+            ds.take_frame(L)
+    el = time.perf_counter() - t0
+    ds.close()
+    return {"value": round(n_frames * W * H / el / 1e9, 3), "unit": "GPixels/s",
+            "ms_per_frame": round(el / n_frames * 1e3, 3),
+            "path": "add_frame(host) + take_frame(all levels), synchronous, 1 GPU",
+            "frames": n_frames}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,232 @@
+/*
+ * aqz_downsampler.h — C ABI of the MI355X-native multiscale pyramid
+ * downsampler (the acquire-zarr streaming hot path).
+ *
+ * This header is the drop-in boundary.  It replaces the CPU implementation of
+ * `zarr::Downsampler` in the reference
+ * (`src/streaming/downsampler.{hh,cpp}`, v0.8.1).  The `zarr::Downsampler`
+ * class contract (downsampler.hh:11-64) is kept by a thin C++ adapter
+ *  that forwards to the functions below.  Nothing else in the
+ * reference changes: `MultiscaleArray` (multiscale.array.cpp:172-189,
+ * 291-325) keeps calling add_frame/take_frame, and the public
+ * `ZarrStream_*` / `ZarrStreamSettings` surface in include/acquire.zarr.h is
+ * untouched.
+ *
+ * Plain C: no C++ or HIP types cross this boundary.  Streams are passed as
+ * `void*` (a hipStream_t).  Enum-valued arguments take the numeric values of
+ * the reference's `ZarrDataType`, `ZarrDownsamplingMethod` and
+ * `ZarrDimensionType` (include/zarr.types.h:55-97); return values are
+ * `ZarrStatusCode` values (zarr.types.h:13-31).
+ *
+ * Threading: a handle is used by one thread at a time, exactly like the
+ * reference Downsampler, which only the stream's frame-queue consumer job
+ * touches (zarr.stream.cpp:1616-1630).  Every entry point binds the handle's
+ * device first (hipSetDevice), because that consumer thread is not the thread
+ * that created the handle.
+ */
+#ifndef AQZ_DOWNSAMPLER_H
+#define AQZ_DOWNSAMPLER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C"
+{
+#endif
+
+/* Status codes: numerically equal to ZarrStatusCode (zarr.types.h:13-31). */
+#define AQZ_OK 0
+#define AQZ_INVALID_ARGUMENT 1
+#define AQZ_OVERFLOW 2
+#define AQZ_INVALID_INDEX 3
+#define AQZ_NOT_YET_IMPLEMENTED 4
+#define AQZ_INTERNAL_ERROR 5
+#define AQZ_OUT_OF_MEMORY 6
+
+/* ZarrDataType values (zarr.types.h:55-68). */
+#define AQZ_DTYPE_UINT8 0
+#define AQZ_DTYPE_UINT16 1
+#define AQZ_DTYPE_UINT32 2
+#define AQZ_DTYPE_UINT64 3
+#define AQZ_DTYPE_INT8 4
+#define AQZ_DTYPE_INT16 5
+#define AQZ_DTYPE_INT32 6
+#define AQZ_DTYPE_INT64 7
+#define AQZ_DTYPE_FLOAT32 8
+#define AQZ_DTYPE_FLOAT64 9
+#define AQZ_DTYPE_COUNT 10
+
+/* ZarrDownsamplingMethod values (zarr.types.h:90-97). */
+#define AQZ_METHOD_DECIMATE 0
+#define AQZ_METHOD_MEAN 1
+#define AQZ_METHOD_MIN 2
+#define AQZ_METHOD_MAX 3
+#define AQZ_METHOD_COUNT 4
+
+/* ZarrDimensionType values (zarr.types.h:81-88). */
+#define AQZ_DIM_SPACE 0
+#define AQZ_DIM_CHANNEL 1
+#define AQZ_DIM_TIME 2
+#define AQZ_DIM_OTHER 3
+
+/* Upper bounds for the fixed-size tables below. */
+#define AQZ_MAX_DIMS 32
+#define AQZ_MAX_LEVELS 32
+
+/*
+ * One dimension of one pyramid level, in storage order.  Mirrors the numeric
+ * fields of the reference's `ZarrDimension` (array.dimensions.hh:12-43); the
+ * name and unit strings stay with the caller, since the planner only copies
+ * them.
+ */
+typedef struct
+{
+    int32_t type;               /* ZarrDimensionType */
+    uint32_t array_size_px;     /* 0 = unbounded append dimension */
+    uint32_t chunk_size_px;
+    uint32_t shard_size_chunks;
+    double scale;
+} aqz_dimension;
+
+/*
+ * Geometry of one pyramid level as the per-frame state machine needs it.
+ * Derived from the level's dimensions: `width` = last dim, `height` =
+ * second-to-last, `planes` = dim[ndims-3] (downsampler.cpp:311-333).
+ */
+typedef struct
+{
+    uint32_t width;
+    uint32_t height;
+    uint32_t planes;
+} aqz_level_desc;
+
+/*
+ * Level planner: restates `Downsampler::make_writer_configurations_`
+ * (downsampler.cpp:493-597) and `downsample_dimension` (downsampler.cpp:8-37).
+ *
+ * `dims` are the base (level-0) dimensions in storage order, already carrying
+ * the phantom singleton dimension the reference prepends to 2-D arrays
+ * (array.dimensions.cpp:149-152), so ndims >= 3.  `max_levels` = 0 means no
+ * limit (ArrayConfig::max_levels, array.base.hh:56).
+ *
+ * Writes `*n_levels` (total levels including level 0) and, if `out` is
+ * non-NULL, `out[level * ndims + d]` for every level.  `out_cap_levels` is the
+ * number of levels `out` has room for; AQZ_OVERFLOW if too small.
+ */
+int aqz_plan_levels(const aqz_dimension* dims,
+                    uint32_t ndims,
+                    uint32_t max_levels,
+                    aqz_dimension* out,
+                    uint32_t out_cap_levels,
+                    uint32_t* n_levels);
+
+/* Opaque downsampler handle: the device-side replacement of zarr::Downsampler. */
+typedef struct aqz_ds aqz_ds;
+
+/*
+ * Create a downsampler for `n_levels` levels (level 0 = full resolution).
+ * Replaces the constructor `Downsampler(config, method)` (downsampler.cpp:
+ * 249-304): dtype and method are validated here.  `device` is the HIP
+ * ordinal; -1 selects $AQZ_GPU_DEVICE or else the current device.
+ * Allocates all device buffers and pinned staging up front.
+ */
+int aqz_ds_create(const aqz_level_desc* levels,
+                  uint32_t n_levels,
+                  int dtype,
+                  int method,
+                  int device,
+                  aqz_ds** out);
+
+/* Release every device/pinned buffer, stream and event of the handle. */
+void aqz_ds_destroy(aqz_ds* ds);
+
+/*
+ * Add one full-resolution frame from host memory.  Replaces
+ * `Downsampler::add_frame` (downsampler.cpp:306-401): same level cascade, Z
+ * pairing, odd-plane pass-through and emit/no-overwrite rules.
+ * `nbytes` must equal width*height*bytes_of_type at level 0.
+ * The host buffer is read only during the call (it is staged to pinned
+ * memory before return), so the caller may reuse it immediately.
+ * Kernels and device->host copies are queued asynchronously; the level
+ * frames are synchronised in aqz_ds_take_frame.
+ */
+int aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes);
+
+/*
+ * Same as aqz_ds_add_frame for a frame already resident in device memory
+ * (`device_frame` is a device pointer on the handle's device).  The frame
+ * must stay valid until the next call on the handle.
+ */
+int aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes);
+
+/*
+ * Take the cached frame of `level` (1..n_levels-1).  Replaces
+ * `Downsampler::take_frame` (downsampler.cpp:403-414): if a frame is cached
+ * it is copied into `dst` (capacity `cap` bytes), removed from the cache,
+ * `*nbytes` is set and `*has_frame` = 1; otherwise `*has_frame` = 0 and
+ * nothing is written.  Not idempotent.
+ * With `dst` == NULL and has_frame, only `*nbytes` is reported and the frame
+ * stays cached (size query).
+ */
+int aqz_ds_take_frame(aqz_ds* ds,
+                      uint32_t level,
+                      void* dst,
+                      size_t cap,
+                      size_t* nbytes,
+                      int* has_frame);
+
+/*
+ * Device-resident batch path (benchmark / bulk API).  Equivalent to calling
+ * aqz_ds_add_frame on `n_frames` consecutive frames of `device_frames`
+ * (frame i at byte offset i*frame_bytes) followed by take_frame on every
+ * level, except that nothing leaves the device: the k-th frame emitted at
+ * level L is written to `device_out_levels[L] + k * level_bytes(L)`.
+ * `device_out_levels[0]` is ignored.  `out_counts` (optional, n_levels
+ * entries) receives the number of frames emitted per level.
+ * Runs on `hip_stream` (NULL = the handle's own stream) and does not
+ * synchronise; pure-2-D pyramids are one fused launch per 4 levels.
+ */
+int aqz_ds_run_device_batch(aqz_ds* ds,
+                            const void* device_frames,
+                            uint32_t n_frames,
+                            void* const* device_out_levels,
+                            uint32_t* out_counts,
+                            void* hip_stream);
+
+/* Bytes of one frame at `level` (0 on bad level). */
+size_t aqz_ds_level_bytes(const aqz_ds* ds, uint32_t level);
+
+/* Number of levels (including level 0). */
+uint32_t aqz_ds_level_count(const aqz_ds* ds);
+
+/* Bytes of device memory held by the handle (reported separately from the
+ * reference's host memory estimate, acquire.zarr.cpp:216-314). */
+size_t aqz_ds_device_memory_usage(const aqz_ds* ds);
+
+/* Last error message of the handle (never NULL; "" when none). */
+const char* aqz_ds_last_error(const aqz_ds* ds);
+
+/* Last error of a failed aqz_ds_create / aqz_plan_levels on this thread. */
+const char* aqz_last_error(void);
+
+/*
+ * `Downsampler::downsampling_method` (downsampler.cpp:422-437): "decimate",
+ * "local_mean", "local_min", "local_max"; NULL for an invalid method.
+ */
+const char* aqz_method_name(int method);
+
+/*
+ * `Downsampler::get_metadata` (downsampler.cpp:440-485) serialised as a
+ * compact JSON object; NULL for an invalid method.
+ */
+const char* aqz_method_metadata_json(int method);
+
+/* Library version string. */
+const char* aqz_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AQZ_DOWNSAMPLER_H */

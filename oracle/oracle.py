@@ -1,0 +1,192 @@
+"""ctypes front-end of the CPU ORACLE (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker.  The product path
+(acquire-zarr_amd/) never imports it.
+
+The C restatement lives in ds_oracle.c (acquire-zarr v0.8.1
+src/streaming/downsampler.cpp, cited per function there).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle_ds.so")
+
+# numpy dtypes indexed by ZarrDataType value (zarr.types.h:55-68)
+NP_DTYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16,
+             np.int32, np.int64, np.float32, np.float64]
+DTYPE_BY_NAME = {np.dtype(t).name: i for i, t in enumerate(NP_DTYPES)}
+
+DECIMATE, MEAN, MIN, MAX = 0, 1, 2, 3
+SPACE, CHANNEL, TIME, OTHER = 0, 1, 2, 3
+
+
+class Dim(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32),
+                ("array_size_px", ctypes.c_uint32),
+                ("chunk_size_px", ctypes.c_uint32),
+                ("shard_size_chunks", ctypes.c_uint32),
+                ("scale", ctypes.c_double)]
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc only)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32
+        L.oracle_scale_image.argtypes = [ctypes.c_int, ctypes.c_int, vp, sz, sz, vp]
+        L.oracle_average_two_frames.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz]
+        L.oracle_reduce4.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp]
+        L.oracle_reduce2.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp]
+        L.oracle_plan_levels.argtypes = [ctypes.POINTER(Dim), u32, u32,
+                                         ctypes.POINTER(Dim), u32,
+                                         ctypes.POINTER(u32)]
+        L.oracle_ds_create.restype = vp
+        L.oracle_ds_create.argtypes = [ctypes.POINTER(u32)] * 3 + [u32, ctypes.c_int, ctypes.c_int]
+        L.oracle_ds_destroy.argtypes = [vp]
+        L.oracle_ds_add_frame.argtypes = [vp, vp, sz]
+        L.oracle_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz)]
+        L.oracle_ds_level_count.argtypes = [vp, u32]
+        L.oracle_ds_level_count.restype = u32
+        _lib = L
+    return _lib
+
+
+def dtype_code(dt) -> int:
+    return DTYPE_BY_NAME[np.dtype(dt).name]
+
+
+def scale_image(img: np.ndarray, method: int) -> np.ndarray:
+    """One 2x2 level (scale_image<T>, downsampler.cpp:139-206)."""
+    img = np.ascontiguousarray(img)
+    h, w = img.shape
+    out = np.zeros(((h + h % 2) // 2, (w + w % 2) // 2), dtype=img.dtype)
+    rc = lib().oracle_scale_image(dtype_code(img.dtype), method,
+                                  img.ctypes.data, w, h, out.ctypes.data)
+    if rc:
+        raise ValueError("oracle_scale_image failed")
+    return out
+
+
+def average_two_frames(earlier: np.ndarray, current: np.ndarray, method: int) -> np.ndarray:
+    """average_two_frames<T> (downsampler.cpp:208-246): f(earlier, current)."""
+    dst = np.ascontiguousarray(earlier).copy()
+    src = np.ascontiguousarray(current)
+    assert dst.shape == src.shape and dst.dtype == src.dtype
+    rc = lib().oracle_average_two_frames(dtype_code(dst.dtype), method,
+                                         dst.ctypes.data, src.ctypes.data, dst.size)
+    if rc:
+        raise ValueError("oracle_average_two_frames failed")
+    return dst
+
+
+def reduce4(dt, method, a, b, c, d):
+    v = np.array([a, b, c, d], dtype=dt)
+    out = np.zeros(1, dtype=dt)
+    p = v.ctypes.data
+    isz = v.itemsize
+    lib().oracle_reduce4(dtype_code(dt), method, p, p + isz, p + 2 * isz, p + 3 * isz,
+                         out.ctypes.data)
+    return out[0]
+
+
+def reduce2(dt, method, a, b):
+    v = np.array([a, b], dtype=dt)
+    out = np.zeros(1, dtype=dt)
+    lib().oracle_reduce2(dtype_code(dt), method, v.ctypes.data,
+                         v.ctypes.data + v.itemsize, out.ctypes.data)
+    return out[0]
+
+
+def plan_levels(dims, max_levels: int = 0):
+    """make_writer_configurations_ (downsampler.cpp:493-597).
+
+    `dims` is a list of (type, array_size, chunk_size, shard_size[, scale])
+    tuples in storage order with ndims >= 3 (2-D arrays get the phantom
+    singleton dim first, array.dimensions.cpp:149-152).  Returns a list of
+    levels, each a list of (type, size, chunk, shard, scale) tuples.
+    """
+    nd = len(dims)
+    arr = (Dim * nd)(*[Dim(d[0], d[1], d[2], d[3], d[4] if len(d) > 4 else 1.0) for d in dims])
+    n = ctypes.c_uint32(0)
+    rc = lib().oracle_plan_levels(arr, nd, max_levels, None, 0, ctypes.byref(n))
+    if rc:
+        raise ValueError("oracle_plan_levels failed")
+    out = (Dim * (nd * n.value))()
+    rc = lib().oracle_plan_levels(arr, nd, max_levels, out, n.value, ctypes.byref(n))
+    if rc:
+        raise ValueError("oracle_plan_levels failed")
+    return [[(o.type, o.array_size_px, o.chunk_size_px, o.shard_size_chunks, o.scale)
+             for o in out[l * nd:(l + 1) * nd]] for l in range(n.value)]
+
+
+def level_geometry(levels):
+    """(width, height, planes) per level, as Downsampler::add_frame reads them."""
+    return [(lv[-1][1], lv[-2][1], lv[-3][1]) for lv in levels]
+
+
+class OracleDownsampler:
+    """Downsampler::add_frame / take_frame (downsampler.cpp:306-414)."""
+
+    def __init__(self, geometry, dtype, method):
+        self.dtype = np.dtype(dtype)
+        self.geometry = list(geometry)
+        n = len(self.geometry)
+        W = (ctypes.c_uint32 * n)(*[g[0] for g in self.geometry])
+        H = (ctypes.c_uint32 * n)(*[g[1] for g in self.geometry])
+        P = (ctypes.c_uint32 * n)(*[g[2] for g in self.geometry])
+        self._h = lib().oracle_ds_create(W, H, P, n, dtype_code(self.dtype), method)
+        if not self._h:
+            raise ValueError("invalid oracle downsampler arguments")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().oracle_ds_destroy(h)
+            self._h = None
+
+    def add_frame(self, frame: np.ndarray):
+        frame = np.ascontiguousarray(frame, dtype=self.dtype)
+        rc = lib().oracle_ds_add_frame(self._h, frame.ctypes.data, frame.nbytes)
+        if rc:
+            raise RuntimeError("oracle add_frame: frame size mismatch")
+
+    def take_frame(self, level: int):
+        w, h, _ = self.geometry[level]
+        out = np.empty((h, w), dtype=self.dtype)
+        nb = ctypes.c_size_t(0)
+        rc = lib().oracle_ds_take_frame(self._h, level, out.ctypes.data, out.nbytes,
+                                        ctypes.byref(nb))
+        if rc < 0:
+            raise RuntimeError("oracle take_frame failed")
+        return out if rc == 1 else None
+
+    def level_count(self, level: int) -> int:
+        return lib().oracle_ds_level_count(self._h, level)
+
+
+def cascade_2d(frame: np.ndarray, n_levels: int, method: int):
+    """Pure XY pyramid of `n_levels` total levels (levels 1..n-1 returned)."""
+    out = []
+    cur = frame
+    for _ in range(1, n_levels):
+        cur = scale_image(cur, method)
+        out.append(cur)
+    return out

@@ -1,0 +1,75 @@
+"""GPU test helpers: device buffers come from torch (plumbing only); every
+pyramid computation goes through the native library's C ABI."""
+import numpy as np
+
+
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("GPU tests need an AMD GPU (torch.cuda unavailable)")
+    return torch
+
+
+def to_device(arr):
+    torch = torch_cuda()
+    raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1).copy()
+    return torch.from_numpy(raw).to("cuda")
+
+
+def empty_device(nbytes):
+    torch = torch_cuda()
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device="cuda")
+
+
+def from_device(t, dtype, shape):
+    torch_cuda().cuda.synchronize()
+    return t.cpu().numpy().view(dtype).reshape(shape)
+
+
+def random_frames(rng, dtype, shape, specials=True):
+    """Full-range integers; floats spread over many magnitudes with NaN, inf,
+    -0.0 and denormals injected."""
+    dt = np.dtype(dtype)
+    if dt.kind in "ui":
+        info = np.iinfo(dt)
+        return rng.integers(info.min, info.max, size=shape, dtype=dt, endpoint=True)
+    x = rng.standard_normal(shape) * np.exp(rng.uniform(-20, 20, shape))
+    x = x.astype(dt)
+    if specials:
+        flat = x.reshape(-1)
+        n = flat.size
+        k = max(1, n // 200)
+        tiny = np.finfo(dt).tiny
+        for val in (np.nan, np.inf, -np.inf, -0.0, 0.0, tiny / 8, -tiny / 3):
+            idx = rng.integers(0, n, k)
+            flat[idx] = dt.type(val)
+    return x
+
+
+def assert_parity(got, want, ctx=""):
+    """Bit-exact for integers; float32/64 within 1 ulp (NaN positions must
+    match) — the tolerance north_star states.  The kernels are expected to be
+    bit-exact; `exact_fraction` is reported on failure."""
+    assert got.shape == want.shape, f"{ctx}: shape {got.shape} vs {want.shape}"
+    assert got.dtype == want.dtype
+    if got.dtype.kind in "ui":
+        if not np.array_equal(got, want):
+            bad = np.argwhere(got != want)
+            i = tuple(bad[0])
+            raise AssertionError(f"{ctx}: {len(bad)} mismatches, first at {i}: "
+                                 f"{got[i]} vs {want[i]}")
+        return
+    gn, wn = np.isnan(got), np.isnan(want)
+    assert np.array_equal(gn, wn), f"{ctx}: NaN positions differ"
+    g, w = got[~gn], want[~wn]
+    ok = (g == w)
+    if not ok.all():
+        # within one ulp: got is want or one of its two float neighbours
+        up = np.nextafter(w, np.array(np.inf, dtype=w.dtype))
+        dn = np.nextafter(w, np.array(-np.inf, dtype=w.dtype))
+        near = ok | (g == up) | (g == dn)
+        if not near.all():
+            i = int(np.argmin(near))
+            raise AssertionError(f"{ctx}: {int((~near).sum())} values beyond 1 ulp; "
+                                 f"exact fraction {float(ok.mean()):.6f}; first "
+                                 f"{g[i]!r} vs {w[i]!r}")

@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the
+same seeded inputs, plus the reference's known answers and full-size
+properties.  Integers must be bit-exact; floats within 1 ulp (NaN positions
+equal) — and are additionally checked bit-exact where stated."""
+import os
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import kat_runner
+from gpu_util import (assert_parity, empty_device, from_device, random_frames,
+                      to_device, torch_cuda)
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DTYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16,
+          np.int32, np.int64, np.float32, np.float64]
+METHODS = [0, 1, 2, 3]
+
+
+def seed_of(*parts):
+    return zlib.crc32(repr(parts).encode())
+
+
+def halving_geometry(w, h, n_levels, planes=1):
+    geo = [(w, h, planes)]
+    for _ in range(1, n_levels):
+        w, h = (w + 1) // 2, (h + 1) // 2
+        geo.append((w, h, planes))
+    return geo
+
+
+def run_both(aqz, oracle, geo, dtype, method, frames, levels=None):
+    """Feed `frames` through both implementations, taking every level after
+    each frame; returns the two lists of (frame_idx, level, array)."""
+    ds = aqz.Downsampler(geo, dtype, method)
+    ref = oracle.OracleDownsampler(geo, dtype, method)
+    got, want = [], []
+    levels = levels or range(1, len(geo))
+    for i, f in enumerate(frames):
+        ds.add_frame(f)
+        ref.add_frame(f)
+        for L in levels:
+            a = ds.take_frame(L)
+            b = ref.take_frame(L)
+            assert (a is None) == (b is None), f"frame {i} level {L} readiness"
+            if a is not None:
+                got.append((i, L, a))
+                want.append((i, L, b))
+    ds.close()
+    return got, want
+
+
+# ---- reference C++ unit tests, restated against aqz::Downsampler ----------
+
+@pytest.mark.parametrize("name", ["test_downsampler", "test_downsampler_odd_z"])
+def test_cpp_reference_unit_tests(name):
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", name)
+    assert os.path.exists(exe), f"{exe} not built (run __graft_entry__.build())"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ---- golden KATs through the Python binding --------------------------------
+
+KATS = kat_runner.load()
+
+
+@pytest.mark.parametrize("case", KATS["stream"], ids=lambda c: c["name"])
+def test_stream_kats_gpu(aqz, case):
+    def make(case, dtype, method):
+        levels = aqz.plan_levels(kat_runner.full_dims(case))
+        return aqz.Downsampler(aqz.level_geometry(levels), dtype, method)
+    kat_runner.run_stream_case(case, make)
+
+
+# ---- randomized parity, all dtypes x methods -------------------------------
+
+SIZES_2D = [
+    (64, 48, 3),      # reference odd-z frame size, fused cascade
+    (11, 11, 3),      # odd edges, generic path
+    (1000, 600, 5),   # non-power-of-two, boundary tiles in the cascade
+    (2048, 40, 4),    # wide and short: row-edge tiles at every level
+    (37, 1023, 4),    # odd width (generic) and odd heights
+    (520, 520, 6),    # two fused runs (4 + 1 levels)
+]
+
+
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("method", METHODS)
+def test_random_2d_parity(aqz, oracle, dtype, method):
+    rng = np.random.default_rng(seed_of(np.dtype(dtype).name, method))
+    for (w, h, nl) in SIZES_2D:
+        geo = halving_geometry(w, h, nl)
+        frames = [random_frames(rng, dtype, (h, w)) for _ in range(2)]
+        got, want = run_both(aqz, oracle, geo, dtype, method, frames)
+        assert len(got) == 2 * (nl - 1)
+        for (i, L, a), (_, _, b) in zip(got, want):
+            assert_parity(a, b, f"{np.dtype(dtype).name} m{method} {w}x{h} f{i} L{L}")
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64], ids=["f32", "f64"])
+@pytest.mark.parametrize("method", METHODS)
+def test_float_bit_exact(aqz, oracle, dtype, method):
+    """The float path follows the reference's operation order exactly, so it
+    is bit-exact (not merely within 1 ulp), NaN payloads aside."""
+    rng = np.random.default_rng(5 + method)
+    geo = halving_geometry(512, 384, 5)
+    frame = random_frames(rng, dtype, (384, 512))
+    got, want = run_both(aqz, oracle, geo, dtype, method, [frame])
+    ib = np.uint32 if dtype == np.float32 else np.uint64
+    for (_, L, a), (_, _, b) in zip(got, want):
+        m = ~np.isnan(b)
+        assert np.array_equal(a[m].view(ib), b[m].view(ib)), f"level {L}"
+
+
+# ---- Z pairing (3-D) --------------------------------------------------------
+
+VOLUMES = [
+    # (w, h, planes per stack, stacks, level geometry (w,h,planes) list)
+    ("even_z", [(64, 64, 8), (32, 32, 4), (16, 16, 2)], 2),
+    ("odd_z", [(64, 48, 15), (32, 24, 8), (16, 12, 4), (16, 12, 2)], 2),
+    ("z_only", [(40, 30, 6), (40, 30, 3), (40, 30, 2)], 3),
+    ("odd_xy_z", [(33, 17, 5), (17, 9, 3), (9, 5, 2)], 3),
+]
+
+
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("vol", VOLUMES, ids=lambda v: v[0])
+def test_random_3d_parity(aqz, oracle, dtype, method, vol):
+    name, geo, stacks = vol
+    rng = np.random.default_rng(seed_of(name, np.dtype(dtype).name, method))
+    w, h, z = geo[0]
+    frames = [random_frames(rng, dtype, (h, w)) for _ in range(z * stacks)]
+    got, want = run_both(aqz, oracle, geo, dtype, method, frames)
+    assert len(got) == len(want) and len(got) > 0
+    for (i, L, a), (_, _, b) in zip(got, want):
+        assert_parity(a, b, f"{name} {np.dtype(dtype).name} m{method} f{i} L{L}")
+
+
+def test_untaken_frame_is_not_overwritten(aqz, oracle):
+    """emplace_downsampled_frame_ keeps the first untaken frame
+    (downsampler.cpp:599-605)."""
+    geo = halving_geometry(64, 64, 3)
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ds.add_frame(np.full((64, 64), 10, np.uint16))
+    ds.add_frame(np.full((64, 64), 20, np.uint16))
+    assert np.all(ds.take_frame(1) == 10)
+    assert ds.take_frame(1) is None
+    ds.add_frame(np.full((64, 64), 30, np.uint16))
+    assert np.all(ds.take_frame(2) == 10)  # level 2 also kept the first
+    assert np.all(ds.take_frame(1) == 30)
+
+
+# ---- device-resident batch API --------------------------------------------
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32, np.int64],
+                         ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("geo_kind", ["2d", "2d_odd", "3d"])
+def test_device_batch_matches_stream(aqz, oracle, dtype, geo_kind):
+    torch = torch_cuda()
+    rng = np.random.default_rng(42)
+    if geo_kind == "2d":
+        geo = halving_geometry(1024, 512, 5)
+    elif geo_kind == "2d_odd":
+        geo = halving_geometry(1000, 333, 4)
+    else:
+        geo = [(256, 128, 6), (128, 64, 3), (64, 32, 2)]
+    n = 7
+    w, h, _ = geo[0]
+    frames = random_frames(rng, dtype, (n, h, w))
+    bpp = np.dtype(dtype).itemsize
+    d_in = to_device(frames)
+    # oracle stream: every emitted frame per level in order
+    ref = oracle.OracleDownsampler(geo, dtype, 1)
+    expected = {L: [] for L in range(1, len(geo))}
+    for f in frames:
+        ref.add_frame(f)
+        for L in expected:
+            r = ref.take_frame(L)
+            if r is not None:
+                expected[L].append(r)
+    outs = [None] + [empty_device(n * gw * gh * bpp) for gw, gh, _ in geo[1:]]
+    ds = aqz.Downsampler(geo, dtype, 1)
+    counts = ds.run_device_batch(d_in.data_ptr(), n,
+                                 [0] + [o.data_ptr() for o in outs[1:]],
+                                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for L in expected:
+        gw, gh, _ = geo[L]
+        assert counts[L] == len(expected[L])
+        got = from_device(outs[L], dtype, (n, gh, gw))
+        for k, e in enumerate(expected[L]):
+            assert_parity(got[k], e, f"batch {geo_kind} L{L} frame {k}")
+
+
+# ---- headline geometry: full size -----------------------------------------
+
+def test_headline_4096_u16_parity(aqz, oracle):
+    """4096^2 uint16, 5 levels, Mean (BASELINE configs[2]): device batch of 4
+    frames bit-exact against the oracle."""
+    torch = torch_cuda()
+    rng = np.random.default_rng(2024)
+    geo = halving_geometry(4096, 4096, 5)
+    n = 4
+    frames = rng.integers(0, 65536, (n, 4096, 4096), dtype=np.uint16)
+    d_in = to_device(frames)
+    outs = [None] + [empty_device(n * w * h * 2) for w, h, _ in geo[1:]]
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ds.run_device_batch(d_in.data_ptr(), n, [0] + [o.data_ptr() for o in outs[1:]],
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for k in range(n):
+        ref = oracle.cascade_2d(frames[k], 5, 1)
+        for L in range(1, 5):
+            w, h, _ = geo[L]
+            got = from_device(outs[L], np.uint16, (n, h, w))[k]
+            assert_parity(got, ref[L - 1], f"4096 frame {k} L{L}")
+
+
+def test_full_size_properties(aqz):
+    """At the bench size (64 frames of 4096^2 u16) check size-independent
+    properties instead of a full oracle run: Decimate level L is exactly the
+    stride-2^L subsample of the base; Min <= Mean <= Max elementwise at every
+    level (truncating means stay inside the block's range through the
+    cascade)."""
+    torch = torch_cuda()
+    geo = halving_geometry(4096, 4096, 5)
+    n = 64
+    g = torch.Generator(device="cuda").manual_seed(7)
+    d_in = torch.randint(0, 256, (n * 4096 * 4096 * 2,), dtype=torch.uint8,
+                         device="cuda", generator=g)
+    s = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for m in METHODS:
+        outs = [None] + [empty_device(n * w * h * 2) for w, h, _ in geo[1:]]
+        ds = aqz.Downsampler(geo, np.uint16, m)
+        ds.run_device_batch(d_in.data_ptr(), n, [0] + [o.data_ptr() for o in outs[1:]], s)
+        res[m] = outs
+    torch.cuda.synchronize()
+    base = d_in.view(torch.int16).view(n, 4096, 4096)
+    for L in range(1, 5):
+        w, h, _ = geo[L]
+        dec = res[0][L].view(torch.int16).view(n, h, w)
+        assert torch.equal(dec, base[:, ::2 ** L, ::2 ** L])
+        lo = res[2][L].view(torch.int16).view(n, h, w).to(torch.int32) & 0xFFFF
+        mid = res[1][L].view(torch.int16).view(n, h, w).to(torch.int32) & 0xFFFF
+        hi = res[3][L].view(torch.int16).view(n, h, w).to(torch.int32) & 0xFFFF
+        assert bool((lo <= mid).all()) and bool((mid <= hi).all())
