@@ -177,7 +177,7 @@ struct CascadeParams
 // RI rows x CI columns per lane.  CI == 1 means the lane holds one column of
 // a column group spread over SI lanes (only the group's first lane is
 // meaningful); the right-hand neighbour then comes from lane + SI.
-template<typename T, int M, int J, int NL, int RI, int CI, bool EDGE>
+template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE>
 __device__ __forceinline__ void
 cascade_level(const CascadeParams& p,
               const T (&in)[RI][CI],
@@ -186,7 +186,6 @@ cascade_level(const CascadeParams& p,
               uint32_t col0,
               int lane)
 {
-    constexpr int C = 16 / int(sizeof(T));
     constexpr int RO = RI / 2;
     constexpr bool kInLane = CI >= 2;
     constexpr int CO = kInLane ? CI / 2 : 1;
@@ -251,11 +250,13 @@ cascade_level(const CascadeParams& p,
     }
 
     if constexpr (J < NL) {
-        cascade_level<T, M, J + 1, NL, RO, CO, EDGE>(p, out, f, row0, col0, lane);
+        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE>(p, out, f, row0, col0,
+                                                       lane);
     }
 }
 
-template<typename T, int M, int NL, bool EDGE>
+// C = columns per lane (a multiple of 16 bytes of T); NT = non-temporal loads.
+template<typename T, int M, int NL, int C, bool NT, bool EDGE>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
@@ -263,35 +264,43 @@ cascade_unit(const CascadeParams& p,
              uint32_t col0,
              int lane)
 {
-    constexpr int C = 16 / int(sizeof(T));
     constexpr int R = 1 << NL;
+    constexpr int V = C * int(sizeof(T)) / 16; // 16-byte loads per row
     const T* src =
       reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
 
     T v[R][C];
-    // All row loads are issued before any arithmetic: 2^NL outstanding
+    // All row loads are issued before any arithmetic: 2^NL * V outstanding
     // 16-byte loads per lane (1 KiB per wave instruction).
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        bool ok = true;
-        if constexpr (EDGE) {
-            ok = (row0 + r < p.H) && (col0 < p.W);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const uint32_t col = col0 + uint32_t(k) * (16 / sizeof(T));
+            bool ok = true;
+            if constexpr (EDGE) {
+                ok = (row0 + r < p.H) && (col < p.W);
+            }
+            u32x4 q = { 0u, 0u, 0u, 0u };
+            if (ok) {
+                const u32x4* a = reinterpret_cast<const u32x4*>(
+                  src + uint64_t(row0 + r) * p.W + col);
+                if constexpr (NT) {
+                    q = __builtin_nontemporal_load(a);
+                } else {
+                    q = *a;
+                }
+            }
+            __builtin_memcpy(&v[r][k * (16 / sizeof(T))], &q, 16);
         }
-        u32x4 q = { 0u, 0u, 0u, 0u };
-        if (ok) {
-            q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-              src + uint64_t(row0 + r) * p.W + col0));
-        }
-        __builtin_memcpy(&v[r][0], &q, 16);
     }
-    cascade_level<T, M, 1, NL, R, C, EDGE>(p, v, f, row0, col0, lane);
+    cascade_level<T, M, C, 1, NL, R, C, EDGE>(p, v, f, row0, col0, lane);
 }
 
-template<typename T, int M, int NL>
+template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool NT = true>
 __global__ __launch_bounds__(256) void
 cascade_kernel(CascadeParams p)
 {
-    constexpr int C = 16 / int(sizeof(T));
     constexpr int R = 1 << NL;
     const int lane = threadIdx.x & 63;
     const uint32_t wave_in_block =
@@ -312,9 +321,9 @@ cascade_kernel(CascadeParams p)
         const bool interior =
           (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
         if (interior) {
-            cascade_unit<T, M, NL, false>(p, f, row0, col0, lane);
+            cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
         } else {
-            cascade_unit<T, M, NL, true>(p, f, row0, col0, lane);
+            cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
         }
     }
 }

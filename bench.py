@@ -98,8 +98,13 @@ def main():
                      for w, h, _ in geo[1:]]
     out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
     ds = aqz.Downsampler(geo, dtype, method, device=local_rank)
-    stream = torch.cuda.current_stream()
+    # A real (non-null) stream: the kernels run on it and the timing events
+    # are recorded on it.
+    torch.cuda.synchronize()  # inputs were generated on the default stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+    assert sptr, "need a non-null HIP stream"
 
     def step():
         ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)

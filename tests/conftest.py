@@ -8,6 +8,13 @@ import sys
 
 import pytest
 
+# torch (device-buffer plumbing in the GPU tests) must bind its HIP runtime
+# before the native library is loaded, so both share one runtime instance.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:

@@ -73,3 +73,13 @@ def assert_parity(got, want, ctx=""):
             raise AssertionError(f"{ctx}: {int((~near).sum())} values beyond 1 ulp; "
                                  f"exact fraction {float(ok.mean()):.6f}; first "
                                  f"{g[i]!r} vs {w[i]!r}")
+
+
+def launch_stream():
+    """A non-null torch stream handle for the batch API (NULL would select the
+    handle's own stream)."""
+    torch = torch_cuda()
+    torch.cuda.synchronize()  # inputs were produced on the previous stream
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    return s.cuda_stream

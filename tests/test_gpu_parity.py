@@ -10,8 +10,8 @@ import numpy as np
 import pytest
 
 import kat_runner
-from gpu_util import (assert_parity, empty_device, from_device, random_frames,
-                      to_device, torch_cuda)
+from gpu_util import (assert_parity, empty_device, from_device, launch_stream,
+                      random_frames, to_device, torch_cuda)
 
 pytestmark = pytest.mark.gpu
 
@@ -188,7 +188,7 @@ def test_device_batch_matches_stream(aqz, oracle, dtype, geo_kind):
     ds = aqz.Downsampler(geo, dtype, 1)
     counts = ds.run_device_batch(d_in.data_ptr(), n,
                                  [0] + [o.data_ptr() for o in outs[1:]],
-                                 torch.cuda.current_stream().cuda_stream)
+                                 launch_stream())
     torch.cuda.synchronize()
     for L in expected:
         gw, gh, _ = geo[L]
@@ -212,7 +212,7 @@ def test_headline_4096_u16_parity(aqz, oracle):
     outs = [None] + [empty_device(n * w * h * 2) for w, h, _ in geo[1:]]
     ds = aqz.Downsampler(geo, np.uint16, 1)
     ds.run_device_batch(d_in.data_ptr(), n, [0] + [o.data_ptr() for o in outs[1:]],
-                        torch.cuda.current_stream().cuda_stream)
+                        launch_stream())
     torch.cuda.synchronize()
     for k in range(n):
         ref = oracle.cascade_2d(frames[k], 5, 1)
@@ -234,7 +234,7 @@ def test_full_size_properties(aqz):
     g = torch.Generator(device="cuda").manual_seed(7)
     d_in = torch.randint(0, 256, (n * 4096 * 4096 * 2,), dtype=torch.uint8,
                          device="cuda", generator=g)
-    s = torch.cuda.current_stream().cuda_stream
+    s = launch_stream()
     res = {}
     for m in METHODS:
         outs = [None] + [empty_device(n * w * h * 2) for w, h, _ in geo[1:]]

@@ -1,0 +1,272 @@
+// tools/microbench.hip — HBM ceiling and cascade-variant A/B on MI355X.
+//
+// Not part of the product.  Times, interleaved in one process (guide §5.4
+// rule 24), on the headline workload (64 frames of 4096^2 uint16, 5 levels,
+// Mean):
+//   read      : streaming read of the 2 GiB batch (the read-side ceiling)
+//   r3w1      : read 3 x 16 B, write 1 x 16 B per step (the cascade's 3:1
+//               read:write mix with ideal store shapes)
+//   cascade*  : the product kernel and variants (columns per lane, NT loads,
+//               grid cap), every variant checked equal to the product output.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -I include
+//          -I acquire-zarr_amd/csrc tools/microbench.hip -o tools/microbench
+#include "../acquire-zarr_amd/csrc/ds_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                               \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,     \
+                         hipGetErrorString(e_));                               \
+            std::exit(2);                                                      \
+        }                                                                      \
+    } while (0)
+
+namespace aqz {
+namespace {
+
+__global__ void
+fill_kernel(uint32_t* p, uint64_t n, uint32_t seed)
+{
+    for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * blockDim.x) {
+        uint64_t x = (i + seed) * 0x9E3779B97F4A7C15ull;
+        x ^= x >> 29;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 32;
+        p[i] = uint32_t(x);
+    }
+}
+
+__global__ __launch_bounds__(256) void
+read_kernel(const u32x4* p, uint64_t n, uint32_t* sink)
+{
+    uint32_t acc = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+    for (; i + 7 * stride < n; i += 8 * stride) {
+        u32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v[k] = __builtin_nontemporal_load(p + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < n; i += stride)
+        acc ^= p[i].x;
+    if (acc == 0x12345678u)
+        sink[0] = acc;
+}
+
+// read 3 vectors, write one (their xor), like the cascade's 3:1 byte mix
+__global__ __launch_bounds__(256) void
+r3w1_kernel(const u32x4* p, uint64_t n_out, u32x4* out)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n_out;
+         i += stride) {
+        const u32x4 a = __builtin_nontemporal_load(p + 3 * i);
+        const u32x4 b = __builtin_nontemporal_load(p + 3 * i + 1);
+        const u32x4 c = __builtin_nontemporal_load(p + 3 * i + 2);
+        out[i] = a ^ b ^ c;
+    }
+}
+
+template<int C, bool NT>
+__global__ __launch_bounds__(256) void
+cascade_variant(CascadeParams p)
+{
+    using T = uint16_t;
+    constexpr int NL = 4;
+    constexpr int R = 1 << NL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t nwaves = gridDim.x * wpb;
+    for (uint32_t u = blockIdx.x * wpb + wib; u < p.total_units; u += nwaves) {
+        const uint32_t ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        const uint32_t uy = t % p.units_y;
+        const uint32_t f = t / p.units_y;
+        const uint32_t row0 = uy * R;
+        const uint32_t tile_col0 = ux * (64u * C);
+        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+        const bool interior = (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
+        if (interior)
+            cascade_unit<T, kMean, NL, C, NT, false>(p, f, row0, col0, lane);
+        else
+            cascade_unit<T, kMean, NL, C, NT, true>(p, f, row0, col0, lane);
+    }
+}
+
+__global__ void
+count_diff(const uint8_t* a, const uint8_t* b, uint64_t n, unsigned long long* bad)
+{
+    unsigned long long local = 0;
+    for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * blockDim.x)
+        local += a[i] != b[i];
+    if (local)
+        atomicAdd(bad, local);
+}
+
+} // namespace
+} // namespace aqz
+
+using namespace aqz;
+
+int
+main(int argc, char** argv)
+{
+    const uint32_t W = 4096, H = 4096, B = argc > 1 ? std::atoi(argv[1]) : 64;
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 20;
+    const int rounds = 3;
+    const uint64_t frame = uint64_t(W) * H;
+    const uint64_t in_bytes = frame * B * 2;
+
+    uint16_t* d_in;
+    CHECK(hipMalloc(&d_in, in_bytes));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0,
+                       reinterpret_cast<uint32_t*>(d_in), in_bytes / 4, 12345u);
+    uint32_t w[4], h[4];
+    uint64_t lvl_bytes = 0;
+    uint32_t ww = W, hh = H;
+    for (int i = 0; i < 4; ++i) {
+        ww = (ww + 1) / 2;
+        hh = (hh + 1) / 2;
+        w[i] = ww;
+        h[i] = hh;
+        lvl_bytes += uint64_t(ww) * hh * 2;
+    }
+    const uint64_t alg_bytes = in_bytes + lvl_bytes * B;
+
+    auto alloc_outs = [&](std::vector<void*>& o) {
+        o.resize(4);
+        for (int i = 0; i < 4; ++i)
+            CHECK(hipMalloc(&o[i], uint64_t(w[i]) * h[i] * 2 * B));
+    };
+    std::vector<void*> ref_out, var_out;
+    alloc_outs(ref_out);
+    alloc_outs(var_out);
+    uint32_t* sink;
+    CHECK(hipMalloc(&sink, 64));
+    u32x4* r3w1_out;
+    const uint64_t r3w1_n = in_bytes / 16 / 3;
+    CHECK(hipMalloc(&r3w1_out, r3w1_n * 16));
+
+    auto params_for = [&](int C, std::vector<void*>& o) {
+        CascadeParams p{};
+        p.src = reinterpret_cast<const uint8_t*>(d_in);
+        p.src_frame_elems = frame;
+        p.W = W;
+        p.H = H;
+        p.units_x = (W + 64 * C - 1) / (64 * C);
+        p.units_y = (H + 15) / 16;
+        p.total_units = p.units_x * p.units_y * B;
+        for (int i = 0; i < 4; ++i) {
+            p.dst[i] = static_cast<uint8_t*>(o[i]);
+            p.dst_frame_elems[i] = uint64_t(w[i]) * h[i];
+            p.w[i] = w[i];
+            p.h[i] = h[i];
+        }
+        return p;
+    };
+
+    struct Variant
+    {
+        std::string name;
+        uint64_t bytes;
+        std::function<void()> run;
+        bool is_cascade;
+        std::vector<float> us;
+    };
+    std::vector<Variant> vs;
+    vs.push_back({ "read (2 GiB, nt)", in_bytes, [&] {
+                      hipLaunchKernelGGL(read_kernel, dim3(4096), dim3(256), 0, 0,
+                                         reinterpret_cast<const u32x4*>(d_in),
+                                         in_bytes / 16, sink);
+                  }, false, {} });
+    vs.push_back({ "r3w1 (3:1 read:write)", r3w1_n * 64, [&] {
+                      hipLaunchKernelGGL(r3w1_kernel, dim3(8192), dim3(256), 0, 0,
+                                         reinterpret_cast<const u32x4*>(d_in), r3w1_n,
+                                         r3w1_out);
+                  }, false, {} });
+    vs.push_back({ "product launch_cascade", alg_bytes, [&] {
+                      LevelOut o[4];
+                      for (int i = 0; i < 4; ++i)
+                          o[i] = { ref_out[i], uint64_t(w[i]) * h[i], w[i], h[i] };
+                      CHECK(launch_cascade(1, 1, d_in, frame, W, H, o, 4, B, 0));
+                  }, true, {} });
+    auto add_var = [&](const char* name, auto kern, int C, uint32_t cap) {
+        vs.push_back({ name, alg_bytes, [&, kern, C, cap] {
+                          CascadeParams p = params_for(C, var_out);
+                          uint32_t grid = (p.total_units + 3) / 4;
+                          if (cap && grid > cap)
+                              grid = cap;
+                          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, p);
+                      }, true, {} });
+    };
+    add_var("C8 nt", cascade_variant<8, true>, 8, 0);
+    add_var("C8 plain", cascade_variant<8, false>, 8, 0);
+    add_var("C16 nt", cascade_variant<16, true>, 16, 0);
+    add_var("C16 plain", cascade_variant<16, false>, 16, 0);
+    add_var("C8 nt cap2048", cascade_variant<8, true>, 8, 2048);
+    add_var("C8 nt cap6144", cascade_variant<8, true>, 8, 6144);
+    add_var("C16 nt cap4096", cascade_variant<16, true>, 16, 4096);
+
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipDeviceSynchronize());
+    for (auto& v : vs) // warm
+        for (int i = 0; i < 2; ++i)
+            v.run();
+    CHECK(hipDeviceSynchronize());
+    for (int r = 0; r < rounds; ++r) {
+        for (auto& v : vs) {
+            for (int i = 0; i < reps; ++i) {
+                CHECK(hipEventRecord(e0, 0));
+                v.run();
+                CHECK(hipEventRecord(e1, 0));
+                CHECK(hipEventSynchronize(e1));
+                float ms;
+                CHECK(hipEventElapsedTime(&ms, e0, e1));
+                v.us.push_back(ms * 1e3f);
+            }
+        }
+    }
+    unsigned long long* bad;
+    CHECK(hipMalloc(&bad, 8));
+    std::printf("batch %u frames of %ux%u u16, alg bytes %.1f MB\n", B, W, H,
+                alg_bytes / 1e6);
+    for (auto& v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        const float med = v.us[v.us.size() / 2], mn = v.us[0];
+        std::string verdict = "";
+        if (v.is_cascade && v.name != "product launch_cascade") {
+            // re-run this variant and compare to the product output
+            v.run();
+            CHECK(hipMemset(bad, 0, 8));
+            for (int i = 0; i < 4; ++i)
+                hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, 0,
+                                   static_cast<uint8_t*>(var_out[i]),
+                                   static_cast<uint8_t*>(ref_out[i]),
+                                   uint64_t(w[i]) * h[i] * 2 * B, bad);
+            unsigned long long nb;
+            CHECK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
+            verdict = nb ? " MISMATCH" : " (== product)";
+        }
+        std::printf("%-26s median %9.1f us  min %9.1f us  %7.1f GB/s (%.1f%% of 8 TB/s)%s\n",
+                    v.name.c_str(), med, mn, v.bytes / (med * 1e3),
+                    100.0 * v.bytes / (med * 1e3) / 8000.0, verdict.c_str());
+    }
+    return 0;
+}
