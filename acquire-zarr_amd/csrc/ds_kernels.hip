@@ -129,8 +129,20 @@ shfl_down_any(T v, int delta)
     }
 }
 
-// Store N contiguous elements of T as one naturally aligned access.
-template<typename T, int N>
+template<bool NT, typename Q>
+__device__ __forceinline__ void
+store_q(Q* dst, Q q)
+{
+    if constexpr (NT) {
+        __builtin_nontemporal_store(q, dst);
+    } else {
+        *dst = q;
+    }
+}
+
+// Store N contiguous elements of T as one naturally aligned access
+// (optionally non-temporal: write-once pyramid levels).
+template<typename T, int N, bool NT = false>
 __device__ __forceinline__ void
 store_vec(T* dst, const T (&v)[N])
 {
@@ -139,21 +151,23 @@ store_vec(T* dst, const T (&v)[N])
     if constexpr (B == 16) {
         u32x4 q;
         __builtin_memcpy(&q, v, 16);
-        *reinterpret_cast<u32x4*>(dst) = q;
+        store_q<NT>(reinterpret_cast<u32x4*>(dst), q);
     } else if constexpr (B == 8) {
         uint64_t q;
         __builtin_memcpy(&q, v, 8);
-        *reinterpret_cast<uint64_t*>(dst) = q;
+        store_q<NT>(reinterpret_cast<uint64_t*>(dst), q);
     } else if constexpr (B == 4) {
         uint32_t q;
         __builtin_memcpy(&q, v, 4);
-        *reinterpret_cast<uint32_t*>(dst) = q;
+        store_q<NT>(reinterpret_cast<uint32_t*>(dst), q);
     } else if constexpr (B == 2) {
         uint16_t q;
         __builtin_memcpy(&q, v, 2);
-        *reinterpret_cast<uint16_t*>(dst) = q;
+        store_q<NT>(reinterpret_cast<uint16_t*>(dst), q);
     } else {
-        *reinterpret_cast<uint8_t*>(dst) = *reinterpret_cast<const uint8_t*>(v);
+        uint8_t q;
+        __builtin_memcpy(&q, v, 1);
+        store_q<NT>(reinterpret_cast<uint8_t*>(dst), q);
     }
 }
 
@@ -177,7 +191,8 @@ struct CascadeParams
 // RI rows x CI columns per lane.  CI == 1 means the lane holds one column of
 // a column group spread over SI lanes (only the group's first lane is
 // meaningful); the right-hand neighbour then comes from lane + SI.
-template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE>
+template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
+         bool NTS = false>
 __device__ __forceinline__ void
 cascade_level(const CascadeParams& p,
               const T (&in)[RI][CI],
@@ -245,18 +260,22 @@ cascade_level(const CascadeParams& p,
             ok = ok && (rout0 + r < hout) && (cout0 < wout);
         }
         if (ok) {
-            store_vec<T, CO>(dst + uint64_t(rout0 + r) * wout + cout0, out[r]);
+            store_vec<T, CO, NTS>(dst + uint64_t(rout0 + r) * wout + cout0,
+                                  out[r]);
         }
     }
 
     if constexpr (J < NL) {
-        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE>(p, out, f, row0, col0,
-                                                       lane);
+        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE, NTS>(p, out, f, row0,
+                                                            col0, lane);
     }
 }
 
-// C = columns per lane (a multiple of 16 bytes of T); NT = non-temporal loads.
-template<typename T, int M, int NL, int C, bool NT, bool EDGE>
+// C = columns per lane (a multiple of 16 bytes of T); NT / NTS = non-temporal
+// loads / stores.  Every byte of the pyramid is touched exactly once, so both
+// streams are marked non-temporal: measured on MI355X (tools/microbench.hip,
+// profiles/r01) the headline batch drops from ~530 to ~475 us with NT stores.
+template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
@@ -294,7 +313,7 @@ cascade_unit(const CascadeParams& p,
             __builtin_memcpy(&v[r][k * (16 / sizeof(T))], &q, 16);
         }
     }
-    cascade_level<T, M, C, 1, NL, R, C, EDGE>(p, v, f, row0, col0, lane);
+    cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS>(p, v, f, row0, col0, lane);
 }
 
 template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool NT = true>

@@ -57,6 +57,9 @@ def parse():
                    help="frames through the streaming host API (0 disables)")
     p.add_argument("--no-check", action="store_true",
                    help="skip the one-frame oracle spot check")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE traffic passes")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -108,6 +111,14 @@ def main():
 
     def step():
         ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
+
+    if args.pmc_child:
+        # launched under `rocprofv3 --pmc` by measure_traffic(): launches only
+        for _ in range(args.warmup + args.steps):
+            step()
+        torch.cuda.synchronize()
+        ds.close()
+        return
 
     # correctness spot check of one frame against the oracle (rank 0, N=1)
     check = None
@@ -166,6 +177,11 @@ def main():
 
     cpu_baseline = None
     e2e = None
+    if rank == 0 and world == 1 and not args.no_pmc:
+        traffic = measure_traffic(args)
+        if traffic is not None:
+            roofline["traffic"] = traffic["bytes_per_launch"]
+            roofline["traffic_detail"] = traffic
     if rank == 0 and world == 1:
         if args.cpu_seconds > 0:
             cpu_baseline = measure_cpu(dtype, W, H, n_levels, method, args.cpu_seconds,
@@ -200,6 +216,54 @@ def main():
     ds.close()
     if dist:
         dist.destroy_process_group()
+
+
+def measure_traffic(args):
+    """HBM bytes per cascade launch from PMC counters, one counter per
+    rocprofv3 pass (MI355X_MICROARCH.md §HBM / rocprofv3 PMC slots):
+      FETCH_SIZE (KiB) x 1024 x 2  — gfx950 counts half of wide streaming reads
+      WRITE_SIZE (KiB) x 1024      — checked against the known output bytes
+    Skipped (None) when rocprofv3 is absent or bench already runs under a
+    profiler."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="aqz_pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc",
+               "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+               "--workload", args.workload, "--batch", str(args.batch),
+               "--method", args.method, "--steps", "3", "--warmup", "1"]
+        env = dict(os.environ, TMPDIR="/tmp")
+        try:
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True,
+                               timeout=300, cwd="/tmp")
+        except subprocess.TimeoutExpired:
+            return None
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return None
+        per = []
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                if "cascade_kernel" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                    per.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not per:
+            return None
+        vals[counter] = float(np.mean(per[1:] if len(per) > 1 else per))
+    fetch = vals["FETCH_SIZE"] * 1024 * 2
+    write = vals["WRITE_SIZE"] * 1024
+    return {"bytes_per_launch": int(fetch + write), "read_bytes": int(fetch),
+            "write_bytes": int(write), "FETCH_SIZE_KiB": vals["FETCH_SIZE"],
+            "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
+            "correction": "FETCH_SIZE x1024 x2 (gfx950 half-count), WRITE_SIZE x1024"}
 
 
 def measure_cpu(dtype, W, H, n_levels, method, seconds, frame):

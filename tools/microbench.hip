@@ -80,7 +80,7 @@ r3w1_kernel(const u32x4* p, uint64_t n_out, u32x4* out)
     }
 }
 
-template<int C, bool NT>
+template<int C, bool NT, bool NTS>
 __global__ __launch_bounds__(256) void
 cascade_variant(CascadeParams p)
 {
@@ -101,9 +101,104 @@ cascade_variant(CascadeParams p)
         const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
         const bool interior = (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
         if (interior)
-            cascade_unit<T, kMean, NL, C, NT, false>(p, f, row0, col0, lane);
+            cascade_unit<T, kMean, NL, C, NT, false, NTS>(p, f, row0, col0, lane);
         else
-            cascade_unit<T, kMean, NL, C, NT, true>(p, f, row0, col0, lane);
+            cascade_unit<T, kMean, NL, C, NT, true, NTS>(p, f, row0, col0, lane);
+    }
+}
+
+template<int C, bool NT, bool NTS, int WPB = 4, bool COLMAJOR = false>
+__global__ __launch_bounds__(WPB * 64) void
+cascade_variant2(CascadeParams p)
+{
+    using T = uint16_t;
+    constexpr int NL = 4;
+    constexpr int R = 1 << NL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * WPB;
+    for (uint32_t u = blockIdx.x * WPB + wib; u < p.total_units; u += nwaves) {
+        uint32_t ux, uy, f;
+        if constexpr (COLMAJOR) {
+            uy = u % p.units_y;
+            const uint32_t t = u / p.units_y;
+            ux = t % p.units_x;
+            f = t / p.units_x;
+        } else {
+            ux = u % p.units_x;
+            const uint32_t t = u / p.units_x;
+            uy = t % p.units_y;
+            f = t / p.units_y;
+        }
+        const uint32_t row0 = uy * R;
+        const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
+        const T* src = reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
+        T v[R][C];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < C / 8; ++k) {
+                const u32x4* a = reinterpret_cast<const u32x4*>(
+                  src + uint64_t(row0 + r) * p.W + col0 + k * 8);
+                u32x4 q = NT ? __builtin_nontemporal_load(a) : *a;
+                __builtin_memcpy(&v[r][k * 8], &q, 16);
+            }
+        cascade_level<T, kMean, C, 1, NL, R, C, false, NTS>(p, v, f, row0, col0, lane);
+    }
+}
+
+// Persistent waves with the next unit's loads issued before the current
+// unit's reduction/stores (register double buffer).  Interior tiles only.
+template<bool NT, bool NTS>
+__global__ __launch_bounds__(256) void
+cascade_pipelined(CascadeParams p)
+{
+    using T = uint16_t;
+    constexpr int NL = 4, C = 8, R = 16;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * 4;
+    auto coords = [&](uint32_t u, uint32_t& f, uint32_t& row0, uint32_t& col0) {
+        const uint32_t ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        row0 = (t % p.units_y) * R;
+        f = t / p.units_y;
+        col0 = ux * (64u * C) + uint32_t(lane) * C;
+    };
+    auto load = [&](uint32_t u, T (&v)[R][C]) {
+        uint32_t f, row0, col0;
+        coords(u, f, row0, col0);
+        const T* src = reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const u32x4* a =
+              reinterpret_cast<const u32x4*>(src + uint64_t(row0 + r) * p.W + col0);
+            u32x4 q = NT ? __builtin_nontemporal_load(a) : *a;
+            __builtin_memcpy(&v[r][0], &q, 16);
+        }
+    };
+    uint32_t u = blockIdx.x * 4 + wib;
+    if (u >= p.total_units)
+        return;
+    T cur[R][C];
+    load(u, cur);
+    while (true) {
+        const uint32_t nu = u + nwaves;
+        const bool more = nu < p.total_units;
+        T nxt[R][C];
+        if (more)
+            load(nu, nxt);
+        uint32_t f, row0, col0;
+        coords(u, f, row0, col0);
+        cascade_level<T, kMean, C, 1, NL, R, C, false, NTS>(p, cur, f, row0, col0, lane);
+        if (!more)
+            break;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                cur[r][c] = nxt[r][c];
+        u = nu;
     }
 }
 
@@ -214,13 +309,26 @@ main(int argc, char** argv)
                           hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, p);
                       }, true, {} });
     };
-    add_var("C8 nt", cascade_variant<8, true>, 8, 0);
-    add_var("C8 plain", cascade_variant<8, false>, 8, 0);
-    add_var("C16 nt", cascade_variant<16, true>, 16, 0);
-    add_var("C16 plain", cascade_variant<16, false>, 16, 0);
-    add_var("C8 nt cap2048", cascade_variant<8, true>, 8, 2048);
-    add_var("C8 nt cap6144", cascade_variant<8, true>, 8, 6144);
-    add_var("C16 nt cap4096", cascade_variant<16, true>, 16, 4096);
+    add_var("C8 nt, plain stores", cascade_variant<8, true, false>, 8, 0);
+    add_var("C8 plain, nt stores", cascade_variant<8, false, true>, 8, 0);
+    add_var("C16 nt, nt stores", cascade_variant<16, true, true>, 16, 0);
+    add_var("v2 C8 nt ntstore", cascade_variant2<8, true, true>, 8, 0);
+    add_var("v2 C8 nt ntstore colmajor", cascade_variant2<8, true, true, 4, true>, 8, 0);
+    add_var("pipe nt ntstore cap1024", cascade_pipelined<true, true>, 8, 1024);
+    add_var("pipe nt ntstore cap2048", cascade_pipelined<true, true>, 8, 2048);
+    add_var("pipe nt ntstore cap4096", cascade_pipelined<true, true>, 8, 4096);
+    add_var("C8 nt ntstore cap4096", cascade_variant<8, true, true>, 8, 4096);
+    vs.push_back({ "v2 C8 nt ntstore wpb8", alg_bytes, [&] {
+                      CascadeParams p = params_for(8, var_out);
+                      hipLaunchKernelGGL((cascade_variant2<8, true, true, 8>),
+                                         dim3((p.total_units + 7) / 8), dim3(512), 0,
+                                         0, p);
+                  }, true, {} });
+    vs.push_back({ "v2 C8 nt ntstore wpb1", alg_bytes, [&] {
+                      CascadeParams p = params_for(8, var_out);
+                      hipLaunchKernelGGL((cascade_variant2<8, true, true, 1>),
+                                         dim3(p.total_units), dim3(64), 0, 0, p);
+                  }, true, {} });
 
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
