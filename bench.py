@@ -43,6 +43,44 @@ WORKLOADS = {
 }
 
 
+# ---- distributed helpers (covered on CPU by tests/test_distributed.py) ----
+
+def rank_frames(total_frames: int, rank: int, world: int):
+    """Round-robin deal of one acquisition stream over ranks: frame i goes to
+    rank i % world (frames are independent)."""
+    return range(rank, total_frames, world)
+
+
+def timed_region(step, steps: int, dist=None, sync=lambda: None):
+    """Barrier + device sync on both sides of exactly `steps` calls of
+    step(i); returns this rank's wall time in seconds."""
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    if dist is not None:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(value: float, dist=None, device="cpu") -> float:
+    if dist is None:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_gpix(world: int, frames_per_rank: int, W: int, H: int, steps: int,
+                   elapsed_max: float) -> float:
+    """Whole-job base GPixels/s: every rank's frames over the slowest rank."""
+    return world * frames_per_rank * W * H * steps / elapsed_max / 1e9
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -74,11 +112,18 @@ def main():
     aqz = aqz_pkg.load()
     aqz.lib()  # fail loudly if the native library is missing
 
-    torch.cuda.set_device(local_rank)
+    # one GPU per rank; the modulo only matters when rehearsing N>1 on a
+    # smaller box (AQZ_DIST_BACKEND=gloo, ranks sharing a device)
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("AQZ_DIST_BACKEND", "nccl")  # nccl = RCCL
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     W, H, dtype, chunk = WORKLOADS[args.workload]
     method = aqz.METHODS[args.method]
@@ -100,7 +145,7 @@ def main():
     outs = [None] + [torch.empty(B * w * h * bpp, dtype=torch.uint8, device="cuda")
                      for w, h, _ in geo[1:]]
     out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
-    ds = aqz.Downsampler(geo, dtype, method, device=local_rank)
+    ds = aqz.Downsampler(geo, dtype, method, device=device)
     # A real (non-null) stream: the kernels run on it and the timing events
     # are recorded on it.
     torch.cuda.synchronize()  # inputs were generated on the default stream
@@ -142,28 +187,19 @@ def main():
     # per-launch kernel timing with HIP events on the launch stream
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+
+    def timed_step(i):
         evs[i][0].record(stream)
         step()
         evs[i][1].record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    launch_ms = [a.elapsed_time(b) for a, b in evs]
 
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(timed_step, args.steps, dist, torch.cuda.synchronize)
+    launch_ms = [a.elapsed_time(b) for a, b in evs]
+    dev = "cuda" if (dist is not None and dist.get_backend() == "nccl") else "cpu"
+    elapsed = max_over_ranks(elapsed, dist, dev)
 
     ms_per_step = elapsed / args.steps * 1e3
-    pixels = world * B * W * H * args.steps
-    value = pixels / elapsed / 1e9
+    value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
 
     alg_bytes = B * aqz.alg_bytes_per_frame(geo, bpp)  # per launch (one step)
     avg_launch_s = float(np.mean(launch_ms)) / 1e3
@@ -187,7 +223,7 @@ def main():
             cpu_baseline = measure_cpu(dtype, W, H, n_levels, method, args.cpu_seconds,
                                        d_in[:frame_bytes].cpu().numpy().view(dtype))
         if args.e2e_frames > 0:
-            e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, local_rank)
+            e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device)
 
     if rank == 0:
         line = {

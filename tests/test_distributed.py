@@ -1,0 +1,67 @@
+"""CPU, world size 2 over gloo: the multi-GPU bench path's partition and
+timing logic (bench.py helpers) — barrier-bracketed timed region, max over
+ranks, whole-job aggregate, and the round-robin frame deal."""
+import os
+import socket
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 1 is the slow rank: 3 steps x 40 ms vs 3 x 5 ms
+    delay = 0.040 if rank == 1 else 0.005
+    el = bench.timed_region(lambda i: time.sleep(delay), 3, dist)
+    mx = bench.max_over_ranks(el, dist)
+    frames = list(bench.rank_frames(10, rank, world))
+    q.put((rank, el, mx, frames))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_timing_and_partition():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, el0, mx0, f0), (r1, el1, mx1, f1) = res
+    # both ranks agree on the max, and it is the slow rank's region
+    assert mx0 == mx1 == max(el0, el1)
+    assert mx0 >= 0.12
+    # the barrier brackets the region: the fast rank waited for the slow one
+    assert el0 >= 0.10
+    # every frame dealt exactly once, round-robin
+    assert sorted(f0 + f1) == list(range(10))
+    assert f0 == [0, 2, 4, 6, 8] and f1 == [1, 3, 5, 7, 9]
+
+
+def test_aggregate_counts_all_ranks():
+    sys.path.insert(0, ROOT)
+    import bench
+    v1 = bench.aggregate_gpix(1, 64, 4096, 4096, 20, 0.01)
+    v8 = bench.aggregate_gpix(8, 64, 4096, 4096, 20, 0.01)
+    assert v8 == pytest.approx(8 * v1)
+    assert v1 == pytest.approx(64 * 4096 * 4096 * 20 / 0.01 / 1e9)
