@@ -33,6 +33,7 @@ METHODS = {"decimate": DECIMATE, "mean": MEAN, "min": MIN, "max": MAX}
 EXPORTS = (
     "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
+    "aqz_ds_last_batch_kind",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -85,6 +86,8 @@ def lib() -> ctypes.CDLL:
                                     ctypes.POINTER(i32)]
     L.aqz_ds_run_device_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
                                           ctypes.POINTER(u32), vp]
+    L.aqz_ds_last_batch_kind.argtypes = [vp]
+    L.aqz_ds_last_batch_kind.restype = i32
     L.aqz_ds_level_bytes.argtypes = [vp, u32]
     L.aqz_ds_level_bytes.restype = sz
     L.aqz_ds_level_count.argtypes = [vp]
@@ -195,6 +198,10 @@ class Downsampler:
 
     def level_bytes(self, level: int) -> int:
         return lib().aqz_ds_level_bytes(self._h, level)
+
+    def last_batch_kind(self) -> int:
+        """0 per-frame, 1 fused 2-D cascade, 2 fused volume, -1 none."""
+        return lib().aqz_ds_last_batch_kind(self._h)
 
     def device_memory_usage(self) -> int:
         return lib().aqz_ds_device_memory_usage(self._h)

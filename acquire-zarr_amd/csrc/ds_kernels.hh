@@ -8,6 +8,9 @@
 //   * xy_generic — one scale_image<T> level, one output pixel per lane; the
 //                 fallback for widths the vector path cannot tile.
 //   * zpair     — average_two_frames<T> (:208-246), out = f(earlier, current).
+//   * volume    — both of the above fused for pyramids whose levels halve XY
+//                 and Z (3-D stacks): 2^NL planes x 2^NL rows per wave, every
+//                 level written from registers.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -18,6 +21,7 @@
 namespace aqz {
 
 constexpr int kMaxFusedLevels = 4;
+constexpr int kMaxVolumeLevels = 2;
 
 // One output level of a cascade launch.  `frame_elems` is the element stride
 // between consecutive frames of that level (w*h for densely packed batches).
@@ -54,6 +58,27 @@ hipError_t launch_cascade(int dtype,
                           int n_out,
                           uint32_t n_frames,
                           hipStream_t stream);
+
+// Fused 2x2x2 (XY reduce, then Z pair) over `n_planes` consecutive planes for
+// pyramids whose levels all halve both XY and Z; n_planes must be a multiple
+// of 2^n_out, n_out in [1, kMaxVolumeLevels].  Level L receives
+// n_planes >> L frames.
+bool volume_supported(int dtype,
+                      const void* src,
+                      uint32_t W,
+                      uint32_t H,
+                      const LevelOut* outs,
+                      int n_out);
+hipError_t launch_volume(int dtype,
+                         int method,
+                         const void* src,
+                         uint64_t src_frame_elems,
+                         uint32_t W,
+                         uint32_t H,
+                         const LevelOut* outs,
+                         int n_out,
+                         uint32_t n_planes,
+                         hipStream_t stream);
 
 // One XY level, any width/alignment.
 hipError_t launch_xy_generic(int dtype,

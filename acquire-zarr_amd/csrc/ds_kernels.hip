@@ -187,32 +187,29 @@ struct CascadeParams
     uint32_t h[kMaxFusedLevels];
 };
 
-// Level J (1-based within the run) from level J-1 held in registers as
-// RI rows x CI columns per lane.  CI == 1 means the lane holds one column of
-// a column group spread over SI lanes (only the group's first lane is
-// meaningful); the right-hand neighbour then comes from lane + SI.
-template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
-         bool NTS = false>
+// Lanes per column group at level J when each lane starts with C columns.
+template<int C, int J>
+constexpr int kLaneStride = ((1 << J) >= C) ? ((1 << J) / C) : 1;
+
+// One XY level in registers: level J (1-based within the run) from level J-1
+// held as RI rows x CI columns per lane.  CI == 1 means the lane holds one
+// column of a column group spread over kLaneStride<C, J-1> lanes (only the
+// group's first lane is meaningful); the right-hand neighbour then comes
+// from that many lanes up.  `win`/`hin` are level J-1's size, `cin0`/`rin0`
+// the lane's first column/row there (edge replication needs them).
+template<typename T, int M, int C, int J, int RI, int CI, bool EDGE>
 __device__ __forceinline__ void
-cascade_level(const CascadeParams& p,
-              const T (&in)[RI][CI],
-              uint32_t f,
-              uint32_t row0,
-              uint32_t col0,
-              int lane)
+xy_step(const T (&in)[RI][CI],
+        T (&out)[RI / 2][(CI >= 2) ? CI / 2 : 1],
+        uint32_t win,
+        uint32_t hin,
+        uint32_t cin0,
+        uint32_t rin0)
 {
     constexpr int RO = RI / 2;
     constexpr bool kInLane = CI >= 2;
     constexpr int CO = kInLane ? CI / 2 : 1;
-    constexpr int SI = ((1 << (J - 1)) >= C) ? ((1 << (J - 1)) / C) : 1;
-    constexpr int SO = ((1 << J) >= C) ? ((1 << J) / C) : 1;
-
-    const uint32_t win = (J == 1) ? p.W : p.w[J - 2];
-    const uint32_t hin = (J == 1) ? p.H : p.h[J - 2];
-    const uint32_t cin0 = col0 >> (J - 1);
-    const uint32_t rin0 = row0 >> (J - 1);
-
-    T out[RO][CO];
+    constexpr int SI = kLaneStride<C, J - 1>;
 #pragma unroll
     for (int r = 0; r < RO; ++r) {
 #pragma unroll
@@ -245,14 +242,24 @@ cascade_level(const CascadeParams& p,
             out[r][c] = reduce4<T, M>(here, right, down, diag);
         }
     }
+}
 
-    const uint32_t wout = p.w[J - 1];
-    const uint32_t hout = p.h[J - 1];
+// Write the lane's RO x CO block of level J (frame base `dst`, row pitch
+// `wout`); only column-group leaders store, edge tiles clip to the level.
+template<typename T, int C, int J, int RO, int CO, bool EDGE, bool NTS>
+__device__ __forceinline__ void
+store_level(T* dst,
+            const T (&out)[RO][CO],
+            uint32_t wout,
+            uint32_t hout,
+            uint32_t col0,
+            uint32_t row0,
+            int lane)
+{
+    constexpr int SO = kLaneStride<C, J>;
     const uint32_t cout0 = col0 >> J;
     const uint32_t rout0 = row0 >> J;
     const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
-    T* dst = reinterpret_cast<T*>(p.dst[J - 1]) +
-             uint64_t(f) * p.dst_frame_elems[J - 1];
 #pragma unroll
     for (int r = 0; r < RO; ++r) {
         bool ok = leader;
@@ -264,7 +271,31 @@ cascade_level(const CascadeParams& p,
                                   out[r]);
         }
     }
+}
 
+// Level J of the 2-D cascade: reduce, store, recurse to J+1.
+template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
+         bool NTS = false>
+__device__ __forceinline__ void
+cascade_level(const CascadeParams& p,
+              const T (&in)[RI][CI],
+              uint32_t f,
+              uint32_t row0,
+              uint32_t col0,
+              int lane)
+{
+    constexpr int RO = RI / 2;
+    constexpr int CO = (CI >= 2) ? CI / 2 : 1;
+    const uint32_t win = (J == 1) ? p.W : p.w[J - 2];
+    const uint32_t hin = (J == 1) ? p.H : p.h[J - 2];
+
+    T out[RO][CO];
+    xy_step<T, M, C, J, RI, CI, EDGE>(in, out, win, hin, col0 >> (J - 1),
+                                      row0 >> (J - 1));
+    T* dst = reinterpret_cast<T*>(p.dst[J - 1]) +
+             uint64_t(f) * p.dst_frame_elems[J - 1];
+    store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
+                                            col0, row0, lane);
     if constexpr (J < NL) {
         cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE, NTS>(p, out, f, row0,
                                                             col0, lane);
@@ -343,6 +374,140 @@ cascade_kernel(CascadeParams p)
             cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
         } else {
             cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
+        }
+    }
+}
+
+// ---- fused volume (2x2x2, two-stage) ----------------------------------------
+//
+// For pyramids whose every level halves XY *and* Z (3-D stacks, BASELINE
+// config V): the reference reduces each plane 2x2 in XY (scale_image), then
+// pairs consecutive reduced planes (average_two_frames, dst = earlier plane,
+// src = current) — two truncations, not an 8-way mean.
+// One wave owns 2^NL planes x 2^NL rows x (64 lanes x 16 B) and produces
+// every level of the run from registers.
+
+struct VolumeParams
+{
+    const uint8_t* src;
+    uint64_t src_frame_elems;
+    uint32_t W, H;
+    uint32_t units_x;
+    uint32_t units_y;
+    uint32_t total_units; // units_x * units_y * plane groups
+    uint8_t* dst[kMaxVolumeLevels];
+    uint64_t dst_frame_elems[kMaxVolumeLevels];
+    uint32_t w[kMaxVolumeLevels];
+    uint32_t h[kMaxVolumeLevels];
+};
+
+template<typename T, int M, int C, int J, int NL, int ZI, int RI, int CI,
+         bool EDGE, bool NTS>
+__device__ __forceinline__ void
+volume_level(const VolumeParams& p,
+             const T (&in)[ZI][RI][CI],
+             uint32_t g,
+             uint32_t row0,
+             uint32_t col0,
+             int lane)
+{
+    constexpr int RO = RI / 2;
+    constexpr int CO = (CI >= 2) ? CI / 2 : 1;
+    constexpr int ZO = ZI / 2;
+    const uint32_t win = (J == 1) ? p.W : p.w[J - 2];
+    const uint32_t hin = (J == 1) ? p.H : p.h[J - 2];
+
+    T xy[ZI][RO][CO];
+#pragma unroll
+    for (int z = 0; z < ZI; ++z) {
+        xy_step<T, M, C, J, RI, CI, EDGE>(in[z], xy[z], win, hin,
+                                          col0 >> (J - 1), row0 >> (J - 1));
+    }
+    T out[ZO][RO][CO];
+#pragma unroll
+    for (int z = 0; z < ZO; ++z) {
+#pragma unroll
+        for (int r = 0; r < RO; ++r) {
+#pragma unroll
+            for (int c = 0; c < CO; ++c) {
+                out[z][r][c] = reduce2<T, M>(xy[2 * z][r][c], xy[2 * z + 1][r][c]);
+            }
+        }
+    }
+#pragma unroll
+    for (int z = 0; z < ZO; ++z) {
+        // level-J frame index: plane group g covers 2^(NL-J) frames there
+        T* dst = reinterpret_cast<T*>(p.dst[J - 1]) +
+                 (uint64_t(g) * ZO + z) * p.dst_frame_elems[J - 1];
+        store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out[z], p.w[J - 1],
+                                                p.h[J - 1], col0, row0, lane);
+    }
+    if constexpr (J < NL) {
+        volume_level<T, M, C, J + 1, NL, ZO, RO, CO, EDGE, NTS>(p, out, g, row0,
+                                                               col0, lane);
+    }
+}
+
+template<typename T, int M, int NL, bool EDGE>
+__device__ __forceinline__ void
+volume_unit(const VolumeParams& p,
+            uint32_t g,
+            uint32_t row0,
+            uint32_t col0,
+            int lane)
+{
+    constexpr int C = 16 / int(sizeof(T));
+    constexpr int R = 1 << NL;
+    constexpr int Z = 1 << NL;
+    T v[Z][R][C];
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+        const T* src = reinterpret_cast<const T*>(p.src) +
+                       (uint64_t(g) * Z + z) * p.src_frame_elems;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            bool ok = true;
+            if constexpr (EDGE) {
+                ok = (row0 + r < p.H) && (col0 < p.W);
+            }
+            u32x4 q = { 0u, 0u, 0u, 0u };
+            if (ok) {
+                q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                  src + uint64_t(row0 + r) * p.W + col0));
+            }
+            __builtin_memcpy(&v[z][r][0], &q, 16);
+        }
+    }
+    volume_level<T, M, C, 1, NL, Z, R, C, EDGE, true>(p, v, g, row0, col0, lane);
+}
+
+template<typename T, int M, int NL>
+__global__ __launch_bounds__(256) void
+volume_kernel(VolumeParams p)
+{
+    constexpr int C = 16 / int(sizeof(T));
+    constexpr int R = 1 << NL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave_in_block =
+      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t waves_per_block = blockDim.x >> 6;
+    const uint32_t nwaves = gridDim.x * waves_per_block;
+    for (uint32_t u = blockIdx.x * waves_per_block + wave_in_block;
+         u < p.total_units;
+         u += nwaves) {
+        const uint32_t ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        const uint32_t uy = t % p.units_y;
+        const uint32_t g = t / p.units_y;
+        const uint32_t row0 = uy * R;
+        const uint32_t tile_col0 = ux * (64u * C);
+        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+        const bool interior =
+          (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
+        if (interior) {
+            volume_unit<T, M, NL, false>(p, g, row0, col0, lane);
+        } else {
+            volume_unit<T, M, NL, true>(p, g, row0, col0, lane);
         }
     }
 }
@@ -605,6 +770,71 @@ launch_cascade(int dtype,
                                        dim3(grid), dim3(256), 0, stream, p);
                     break;
             }
+            return hipGetLastError();
+        });
+    });
+}
+
+bool
+volume_supported(int dtype,
+                 const void* src,
+                 uint32_t W,
+                 uint32_t H,
+                 const LevelOut* outs,
+                 int n_out)
+{
+    return n_out >= 1 && n_out <= kMaxVolumeLevels &&
+           cascade_supported(dtype, src, W, H, outs, n_out);
+}
+
+hipError_t
+launch_volume(int dtype,
+              int method,
+              const void* src,
+              uint64_t src_frame_elems,
+              uint32_t W,
+              uint32_t H,
+              const LevelOut* outs,
+              int n_out,
+              uint32_t n_planes,
+              hipStream_t stream)
+{
+    if (!volume_supported(dtype, src, W, H, outs, n_out) || n_planes == 0 ||
+        n_planes % (1u << n_out) != 0)
+        return hipErrorInvalidValue;
+    if ((src_frame_elems * dtype_bytes(dtype)) % 16 != 0)
+        return hipErrorInvalidValue;
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        constexpr uint32_t C = 16 / sizeof(T);
+        VolumeParams p{};
+        p.src = static_cast<const uint8_t*>(src);
+        p.src_frame_elems = src_frame_elems;
+        p.W = W;
+        p.H = H;
+        const uint32_t R = 1u << n_out;
+        p.units_x = (W + 64 * C - 1) / (64 * C);
+        p.units_y = (H + R - 1) / R;
+        const uint64_t total =
+          uint64_t(p.units_x) * p.units_y * (n_planes >> n_out);
+        if (total >= (1ull << 31))
+            return hipErrorInvalidValue;
+        p.total_units = uint32_t(total);
+        for (int i = 0; i < n_out; ++i) {
+            p.dst[i] = static_cast<uint8_t*>(outs[i].ptr);
+            p.dst_frame_elems[i] = outs[i].frame_elems;
+            p.w[i] = outs[i].w;
+            p.h[i] = outs[i].h;
+        }
+        const uint32_t grid = grid_for(total, 4, 0);
+        return with_method(method, [&](auto mtag) -> hipError_t {
+            constexpr int M = decltype(mtag)::value;
+            if (n_out == 1)
+                hipLaunchKernelGGL((volume_kernel<T, M, 1>), dim3(grid),
+                                   dim3(256), 0, stream, p);
+            else
+                hipLaunchKernelGGL((volume_kernel<T, M, 2>), dim3(grid),
+                                   dim3(256), 0, stream, p);
             return hipGetLastError();
         });
     });

@@ -93,6 +93,7 @@ struct aqz_ds
     std::vector<uint8_t> cached;
     std::vector<hipEvent_t> ready;
     size_t device_bytes = 0;
+    int last_batch_kind = -1;
 
     std::string err;
 
@@ -591,55 +592,81 @@ aqz_ds_run_device_batch(aqz_ds* ds,
     int rc = AQZ_OK;
 
     bool pure_xy = ds->n > 1;
-    for (uint32_t l = 1; l < ds->n; ++l)
+    bool pure_xyz = ds->n > 1;
+    for (uint32_t l = 1; l < ds->n; ++l) {
         pure_xy = pure_xy && ds->xy[l] && !ds->zh[l];
+        // every level halves XY and Z, no odd stack (no pass-through plane)
+        // and no stored earlier plane: planes pair up consecutively
+        pure_xyz = pure_xyz && ds->xy[l] && ds->zh[l] &&
+                   ds->lv[l - 1].planes % 2 == 0 && !ds->has_partial[l];
+    }
+    pure_xyz = pure_xyz && n_frames > 0 && (n_frames % (1u << (ds->n - 1))) == 0;
 
-    aqz::LevelOut outs[aqz::kMaxFusedLevels];
-    const uint32_t k0 = std::min<uint32_t>(ds->n - 1, aqz::kMaxFusedLevels);
-    for (uint32_t j = 0; pure_xy && j < k0; ++j)
-        outs[j] = { device_out_levels[1 + j], elems(ds, 1 + j),
-                    ds->lv[1 + j].width, ds->lv[1 + j].height };
-
-    if (pure_xy && n_frames > 0 &&
-        aqz::cascade_supported(ds->dtype, device_frames, ds->lv[0].width,
-                               ds->lv[0].height, outs, int(k0))) {
-        // Whole batch, every frame independent: one launch per 4 levels.
-        uint32_t L = 1;
+    // Plan fused runs (up to `maxk` levels per launch) and check that every
+    // run can take the vector path before launching anything.
+    auto plan_runs = [&](uint32_t maxk, bool volume) {
+        std::vector<std::pair<uint32_t, uint32_t>> runs; // (first level, count)
         const void* src = device_frames;
-        while (L < ds->n && rc == AQZ_OK) {
-            const uint32_t k = std::min<uint32_t>(ds->n - L, aqz::kMaxFusedLevels);
+        for (uint32_t L = 1; L < ds->n;) {
+            const uint32_t k = std::min<uint32_t>(ds->n - L, maxk);
+            aqz::LevelOut o[aqz::kMaxFusedLevels];
             for (uint32_t j = 0; j < k; ++j)
-                outs[j] = { device_out_levels[L + j], elems(ds, L + j),
-                            ds->lv[L + j].width, ds->lv[L + j].height };
+                o[j] = { device_out_levels[L + j], elems(ds, L + j),
+                         ds->lv[L + j].width, ds->lv[L + j].height };
             const aqz_level_desc& a = ds->lv[L - 1];
-            hipError_t e;
-            if (aqz::cascade_supported(ds->dtype, src, a.width, a.height, outs,
-                                       int(k))) {
-                e = aqz::launch_cascade(ds->dtype, ds->method, src,
-                                        elems(ds, L - 1), a.width, a.height,
-                                        outs, int(k), n_frames, ds->stream);
-            } else {
-                e = hipSuccess;
-                const void* s = src;
-                for (uint32_t j = 0; j < k && e == hipSuccess; ++j) {
-                    const aqz_level_desc& b = ds->lv[L + j - 1];
-                    e = aqz::launch_xy_generic(ds->dtype, ds->method, s,
-                                               elems(ds, L + j - 1), b.width,
-                                               b.height, outs[j], n_frames,
-                                               ds->stream);
-                    s = outs[j].ptr;
-                }
-            }
-            if (e != hipSuccess)
-                rc = ds->fail(e, "batch cascade");
-            src = outs[k - 1].ptr;
+            const bool ok =
+              volume ? aqz::volume_supported(ds->dtype, src, a.width, a.height, o, int(k))
+                     : aqz::cascade_supported(ds->dtype, src, a.width, a.height, o, int(k));
+            if (!ok)
+                return std::vector<std::pair<uint32_t, uint32_t>>{};
+            runs.emplace_back(L, k);
+            src = o[k - 1].ptr;
             L += k;
         }
-        for (uint32_t l = 0; l < ds->n; ++l) {
-            ds->count[l] += n_frames;
-            emitted[l] = n_frames;
+        return runs;
+    };
+
+    std::vector<std::pair<uint32_t, uint32_t>> runs;
+    bool volume = false;
+    if (pure_xy && n_frames > 0) {
+        runs = plan_runs(aqz::kMaxFusedLevels, false);
+    } else if (pure_xyz) {
+        runs = plan_runs(aqz::kMaxVolumeLevels, true);
+        volume = true;
+    }
+
+    if (!runs.empty()) {
+        // Whole batch in fused launches; every frame / plane group independent.
+        const void* src = device_frames;
+        uint32_t planes = n_frames;
+        for (const auto& [L, k] : runs) {
+            aqz::LevelOut o[aqz::kMaxFusedLevels];
+            for (uint32_t j = 0; j < k; ++j)
+                o[j] = { device_out_levels[L + j], elems(ds, L + j),
+                         ds->lv[L + j].width, ds->lv[L + j].height };
+            const aqz_level_desc& a = ds->lv[L - 1];
+            const hipError_t e =
+              volume ? aqz::launch_volume(ds->dtype, ds->method, src,
+                                          elems(ds, L - 1), a.width, a.height, o,
+                                          int(k), planes, ds->stream)
+                     : aqz::launch_cascade(ds->dtype, ds->method, src,
+                                           elems(ds, L - 1), a.width, a.height, o,
+                                           int(k), n_frames, ds->stream);
+            if (e != hipSuccess) {
+                rc = ds->fail(e, volume ? "batch volume" : "batch cascade");
+                break;
+            }
+            src = o[k - 1].ptr;
+            if (volume)
+                planes >>= k;
         }
+        for (uint32_t l = 0; l < ds->n; ++l) {
+            emitted[l] = volume ? (n_frames >> l) : n_frames;
+            ds->count[l] += emitted[l];
+        }
+        ds->last_batch_kind = volume ? 2 : 1;
     } else {
+        ds->last_batch_kind = 0;
         Sink sink;
         sink.batch = true;
         sink.out = device_out_levels;
@@ -653,6 +680,12 @@ aqz_ds_run_device_batch(aqz_ds* ds,
         std::copy(emitted.begin(), emitted.end(), out_counts);
     ds->stream = saved;
     return rc;
+}
+
+int
+aqz_ds_last_batch_kind(const aqz_ds* ds)
+{
+    return ds ? ds->last_batch_kind : -1;
 }
 
 size_t

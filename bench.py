@@ -35,12 +35,15 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 WORKLOADS = {
-    # name: (width, height, dtype, chunk) — levels come from the planner
-    "4096x4096_u16": (4096, 4096, np.uint16, 256),   # headline, configs[2]
-    "2048x2048_u16": (2048, 2048, np.uint16, 256),   # configs[1]
-    "4096x4096_f32": (4096, 4096, np.float32, 256),  # configs[3] (per GPU)
-    "512x512_u8": (512, 512, np.uint8, 128),         # configs[0] synthetic
+    # name: (width, height, planes, dtype, xy chunk, z chunk, frames per step)
+    # planes = 0: 2-D frames; levels always come from the planner.
+    "4096x4096_u16": (4096, 4096, 0, np.uint16, 256, 0, 64),     # headline, configs[2]
+    "2048x2048_u16": (2048, 2048, 0, np.uint16, 256, 0, 64),     # configs[1]
+    "4096x4096_f32": (4096, 4096, 0, np.float32, 256, 0, 64),    # configs[3] (per GPU)
+    "512x512_u8": (512, 512, 0, np.uint8, 128, 0, 64),           # configs[0] synthetic
+    "1024x1024x256_u16": (1024, 1024, 256, np.uint16, 256, 64, 256),  # configs[4]
 }
+HEADLINE_METRIC = "GPixels/s device-resident multiscale downsample, 4096² uint16, 5 levels"
 
 
 # ---- distributed helpers (covered on CPU by tests/test_distributed.py) ----
@@ -87,7 +90,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="4096x4096_u16", choices=sorted(WORKLOADS))
-    p.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    p.add_argument("--batch", type=int, default=0,
+                   help="frames (planes) per step per GPU; 0 = workload default")
     p.add_argument("--method", default="mean", choices=["decimate", "mean", "min", "max"])
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (0 disables)")
@@ -125,13 +129,16 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    W, H, dtype, chunk = WORKLOADS[args.workload]
+    W, H, Z, dtype, chunk, zchunk, default_batch = WORKLOADS[args.workload]
     method = aqz.METHODS[args.method]
-    dims = [(aqz.TIME, 0, 1, 1), (aqz.SPACE, H, chunk, 1), (aqz.SPACE, W, chunk, 1)]
+    dims = [(aqz.TIME, 0, 1, 1)]
+    if Z:
+        dims.append((aqz.SPACE, Z, zchunk, 1))
+    dims += [(aqz.SPACE, H, chunk, 1), (aqz.SPACE, W, chunk, 1)]
     geo = aqz.level_geometry(aqz.plan_levels(dims))
     n_levels = len(geo)
     bpp = np.dtype(dtype).itemsize
-    B = args.batch
+    B = args.batch or default_batch
     frame_bytes = W * H * bpp
 
     # synthetic input, resident in HBM before timing (seeded per rank)
@@ -154,8 +161,10 @@ def main():
     sptr = stream.cuda_stream
     assert sptr, "need a non-null HIP stream"
 
+    counts = [0] * n_levels
+
     def step():
-        ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
+        counts[:] = ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
 
     if args.pmc_child:
         # launched under `rocprofv3 --pmc` by measure_traffic(): launches only
@@ -171,14 +180,24 @@ def main():
         import oracle as orc_mod  # test infrastructure: checker only
         step()
         torch.cuda.synchronize()
-        f0 = d_in[:frame_bytes].cpu().numpy().view(dtype).reshape(H, W)
-        ref = orc_mod.cascade_2d(f0, n_levels, method)
+        # first 2^(levels-1) frames (one aligned plane group for volumes)
+        nchk = min(B, 1 << (n_levels - 1)) if Z else 1
+        host = d_in[:nchk * frame_bytes].cpu().numpy().view(dtype).reshape(nchk, H, W)
+        ref = orc_mod.OracleDownsampler(geo, dtype, method)
+        emitted = [0] * n_levels
         ok = True
-        for L in range(1, n_levels):
-            w, h, _ = geo[L]
-            got = outs[L][: w * h * bpp].cpu().numpy().view(dtype).reshape(h, w)
-            ok = ok and np.array_equal(got.view(np.uint8), ref[L - 1].view(np.uint8))
-        check = "bit-exact" if ok else "MISMATCH"
+        for i in range(nchk):
+            ref.add_frame(host[i])
+            for L in range(1, n_levels):
+                r = ref.take_frame(L)
+                if r is None:
+                    continue
+                w, h, _ = geo[L]
+                k = emitted[L]
+                got = outs[L][k * w * h * bpp:(k + 1) * w * h * bpp].cpu().numpy()
+                ok = ok and np.array_equal(got, r.view(np.uint8).reshape(-1))
+                emitted[L] += 1
+        check = ("bit-exact" if ok else "MISMATCH") + f" ({nchk} frame(s) vs oracle)"
 
     for _ in range(args.warmup):
         step()
@@ -201,7 +220,13 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
 
-    alg_bytes = B * aqz.alg_bytes_per_frame(geo, bpp)  # per launch (one step)
+    # algorithmic bytes per step: read every input frame once, write every
+    # emitted level frame once (counts from the batch call)
+    alg_bytes = B * frame_bytes + sum(counts[L] * geo[L][0] * geo[L][1] * bpp
+                                      for L in range(1, n_levels))
+    kind = ds.last_batch_kind()  # 1 fused 2-D cascade, 2 fused volume, 0 per-frame
+    per = {1: 4, 2: 2}.get(kind)
+    launches = -(-(n_levels - 1) // per) if per else None
     avg_launch_s = float(np.mean(launch_ms)) / 1e3
     achieved = alg_bytes / avg_launch_s / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -214,7 +239,7 @@ def main():
     cpu_baseline = None
     e2e = None
     if rank == 0 and world == 1 and not args.no_pmc:
-        traffic = measure_traffic(args)
+        traffic = measure_traffic(args, "volume_kernel" if Z else "cascade_kernel")
         if traffic is not None:
             roofline["traffic"] = traffic["bytes_per_launch"]
             roofline["traffic_detail"] = traffic
@@ -226,8 +251,11 @@ def main():
             e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device)
 
     if rank == 0:
+        metric = HEADLINE_METRIC if args.workload == "4096x4096_u16" else (
+            f"GPixels/s device-resident multiscale downsample, {args.workload}, "
+            f"{n_levels} levels")
         line = {
-            "metric": "GPixels/s device-resident multiscale downsample, 4096² uint16, 5 levels",
+            "metric": metric,
             "value": round(value, 2),
             "unit": "GPixels/s",
             "n_gpus": world,
@@ -239,9 +267,13 @@ def main():
             "vs_baseline": None,
             "dtype": np.dtype(dtype).name.replace("uint", "u").replace("float", "f"),
             "data": "synthetic (uniform random, seeded per rank)",
-            "config": {"workload": f"{W}x{H} {np.dtype(dtype).name}, {n_levels} levels, "
+            "config": {"workload": f"{args.workload}: {W}x{H}" + (f"x{Z} volume" if Z else "")
+                                   + f" {np.dtype(dtype).name}, {n_levels} levels, "
                                    f"{args.method}, device-resident batch",
                        "frames_per_step_per_gpu": B, "levels": n_levels,
+                       "launches_per_step": launches,
+                       "batch_path": {0: "per-frame", 1: "fused cascade",
+                                      2: "fused volume"}.get(kind, "?"),
                        "parallelism": f"frame-sharded x{world}, no collective",
                        "check": check},
             "roofline": roofline,
@@ -254,7 +286,7 @@ def main():
         dist.destroy_process_group()
 
 
-def measure_traffic(args):
+def measure_traffic(args, kernel):
     """HBM bytes per cascade launch from PMC counters, one counter per
     rocprofv3 pass (MI355X_MICROARCH.md §HBM / rocprofv3 PMC slots):
       FETCH_SIZE (KiB) x 1024 x 2  — gfx950 counts half of wide streaming reads
@@ -288,7 +320,7 @@ def measure_traffic(args):
         per = []
         with open(files[0]) as f:
             for row in csv.DictReader(f):
-                if "cascade_kernel" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
                     per.append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not per:

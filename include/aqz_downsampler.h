@@ -194,6 +194,13 @@ int aqz_ds_run_device_batch(aqz_ds* ds,
                             uint32_t* out_counts,
                             void* hip_stream);
 
+/*
+ * Diagnostic: the path the last aqz_ds_run_device_batch took —
+ * 0 = per-frame state machine, 1 = fused 2-D cascade, 2 = fused volume
+ * (XY + Z), -1 = none yet.
+ */
+int aqz_ds_last_batch_kind(const aqz_ds* ds);
+
 /* Bytes of one frame at `level` (0 on bad level). */
 size_t aqz_ds_level_bytes(const aqz_ds* ds, uint32_t level);
 

@@ -158,25 +158,32 @@ def test_untaken_frame_is_not_overwritten(aqz, oracle):
 
 # ---- device-resident batch API --------------------------------------------
 
+BATCH_GEOMETRIES = {
+    # name: (geometry, frames in the batch, expected batch path)
+    "2d": (halving_geometry(1024, 512, 5), 7, 1),
+    "2d_odd": (halving_geometry(1000, 333, 4), 7, 1),
+    "2d_generic": (halving_geometry(1001, 333, 3), 5, 0),               # odd width
+    "3d_odd_stack": ([(256, 128, 6), (128, 64, 3), (64, 32, 2)], 7, 0),  # per-frame
+    "3d_fused": ([(256, 128, 8), (128, 64, 4), (64, 32, 2)], 8, 2),      # volume
+    "3d_fused_deep": ([(512, 256, 16), (256, 128, 8), (128, 64, 4), (64, 32, 2)], 16, 2),
+    "3d_fused_edge": ([(200, 61, 8), (100, 31, 4), (50, 16, 2)], 8, 2),  # odd rows
+}
+
+
 @pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32, np.int64],
                          ids=lambda d: np.dtype(d).name)
-@pytest.mark.parametrize("geo_kind", ["2d", "2d_odd", "3d"])
-def test_device_batch_matches_stream(aqz, oracle, dtype, geo_kind):
+@pytest.mark.parametrize("method", [0, 1, 2, 3])
+@pytest.mark.parametrize("geo_kind", sorted(BATCH_GEOMETRIES))
+def test_device_batch_matches_stream(aqz, oracle, dtype, method, geo_kind):
     torch = torch_cuda()
-    rng = np.random.default_rng(42)
-    if geo_kind == "2d":
-        geo = halving_geometry(1024, 512, 5)
-    elif geo_kind == "2d_odd":
-        geo = halving_geometry(1000, 333, 4)
-    else:
-        geo = [(256, 128, 6), (128, 64, 3), (64, 32, 2)]
-    n = 7
+    rng = np.random.default_rng(seed_of(geo_kind, np.dtype(dtype).name, method))
+    geo, n, kind = BATCH_GEOMETRIES[geo_kind]
     w, h, _ = geo[0]
     frames = random_frames(rng, dtype, (n, h, w))
     bpp = np.dtype(dtype).itemsize
     d_in = to_device(frames)
     # oracle stream: every emitted frame per level in order
-    ref = oracle.OracleDownsampler(geo, dtype, 1)
+    ref = oracle.OracleDownsampler(geo, dtype, method)
     expected = {L: [] for L in range(1, len(geo))}
     for f in frames:
         ref.add_frame(f)
@@ -185,11 +192,12 @@ def test_device_batch_matches_stream(aqz, oracle, dtype, geo_kind):
             if r is not None:
                 expected[L].append(r)
     outs = [None] + [empty_device(n * gw * gh * bpp) for gw, gh, _ in geo[1:]]
-    ds = aqz.Downsampler(geo, dtype, 1)
+    ds = aqz.Downsampler(geo, dtype, method)
     counts = ds.run_device_batch(d_in.data_ptr(), n,
                                  [0] + [o.data_ptr() for o in outs[1:]],
                                  launch_stream())
     torch.cuda.synchronize()
+    assert ds.last_batch_kind() == kind
     for L in expected:
         gw, gh, _ = geo[L]
         assert counts[L] == len(expected[L])
