@@ -20,6 +20,7 @@
 // from the same pass, so the base frame is read exactly once.
 #include "ds_kernels.hh"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace aqz {
@@ -692,9 +693,8 @@ cascade_supported(int dtype,
     if (!b || n_out < 1 || n_out > kMaxFusedLevels || W == 0 || H == 0)
         return false;
     const uint32_t C = uint32_t(16 / b);
-    if (W % C != 0)
-        return false;
-    if (reinterpret_cast<uintptr_t>(src) % 16 != 0)
+    // 16-byte row loads: every row start is 16-byte aligned iff W % C == 0
+    if (W % C != 0 || reinterpret_cast<uintptr_t>(src) % 16 != 0)
         return false;
     uint32_t w = W, h = H;
     for (int i = 0; i < n_out; ++i) {
@@ -702,9 +702,12 @@ cascade_supported(int dtype,
         h = (h + 1) / 2;
         if (outs[i].w != w || outs[i].h != h)
             return false;
-        if (reinterpret_cast<uintptr_t>(outs[i].ptr) % 16 != 0)
+        // level J = i+1 stores max(16 >> J, bpp) bytes per lane; rows are
+        // multiples of that (W % C == 0), so frame base and stride must be too
+        const size_t sw = std::max<size_t>(size_t(16) >> (i + 1), b);
+        if (reinterpret_cast<uintptr_t>(outs[i].ptr) % sw != 0)
             return false;
-        if ((outs[i].frame_elems * b) % 16 != 0)
+        if ((outs[i].frame_elems * b) % sw != 0)
             return false;
     }
     return true;
