@@ -92,7 +92,7 @@ hipError_t launch_xy_generic(int dtype,
                              hipStream_t stream);
 
 // out[i] = reduce2(earlier[i], current[i]) over n elements; `out` may alias
-// either input.
+// either input.  16-byte vectors when all pointers are aligned, else scalar.
 hipError_t launch_zpair(int dtype,
                         int method,
                         void* out,

@@ -550,27 +550,32 @@ xy_generic_kernel(const T* __restrict__ src,
 
 // ---- Z pair ----------------------------------------------------------------
 
-template<typename T, int M>
+template<typename T, int M, bool VEC>
 __global__ __launch_bounds__(256) void
 zpair_kernel(T* out, const T* earlier, const T* current, uint64_t n)
 {
     constexpr int C = 16 / int(sizeof(T));
-    const uint64_t nvec = n / C;
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    for (uint64_t i = tid; i < nvec; i += stride) {
-        const u32x4 qa = reinterpret_cast<const u32x4*>(earlier)[i];
-        const u32x4 qb = reinterpret_cast<const u32x4*>(current)[i];
-        T a[C], b[C], o[C];
-        __builtin_memcpy(a, &qa, 16);
-        __builtin_memcpy(b, &qb, 16);
+    uint64_t done = 0;
+    if constexpr (VEC) {
+        // all three pointers 16-byte aligned: 16 B per lane per operand
+        const uint64_t nvec = n / C;
+        for (uint64_t i = tid; i < nvec; i += stride) {
+            const u32x4 qa = reinterpret_cast<const u32x4*>(earlier)[i];
+            const u32x4 qb = reinterpret_cast<const u32x4*>(current)[i];
+            T a[C], b[C], o[C];
+            __builtin_memcpy(a, &qa, 16);
+            __builtin_memcpy(b, &qb, 16);
 #pragma unroll
-        for (int k = 0; k < C; ++k) {
-            o[k] = reduce2<T, M>(a[k], b[k]);
+            for (int k = 0; k < C; ++k) {
+                o[k] = reduce2<T, M>(a[k], b[k]);
+            }
+            store_vec<T, C>(out + i * C, o);
         }
-        store_vec<T, C>(out + i * C, o);
+        done = nvec * C;
     }
-    for (uint64_t i = nvec * C + tid; i < n; i += stride) {
+    for (uint64_t i = done + tid; i < n; i += stride) {
         out[i] = reduce2<T, M>(earlier[i], current[i]);
     }
 }
@@ -885,24 +890,30 @@ launch_zpair(int dtype,
 {
     if (n == 0)
         return hipSuccess;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(out) |
-                        reinterpret_cast<uintptr_t>(earlier) |
-                        reinterpret_cast<uintptr_t>(current);
-    if (a % 16 != 0)
-        return hipErrorInvalidValue;
     const size_t b = dtype_bytes(dtype);
     if (!b)
         return hipErrorInvalidValue;
-    const uint64_t nvec = (n * b + 15) / 16;
-    const uint32_t grid = grid_for(nvec, 256, 8192);
+    // batch slots of odd-sized levels need not be 16-byte aligned
+    const bool vec = ((reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(earlier) |
+                       reinterpret_cast<uintptr_t>(current)) %
+                      16) == 0;
+    const uint64_t items = vec ? (n * b + 15) / 16 : n;
+    const uint32_t grid = grid_for(items, 256, 8192);
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            hipLaunchKernelGGL((zpair_kernel<T, M>), dim3(grid), dim3(256), 0,
-                               stream, static_cast<T*>(out),
-                               static_cast<const T*>(earlier),
-                               static_cast<const T*>(current), n);
+            if (vec)
+                hipLaunchKernelGGL((zpair_kernel<T, M, true>), dim3(grid),
+                                   dim3(256), 0, stream, static_cast<T*>(out),
+                                   static_cast<const T*>(earlier),
+                                   static_cast<const T*>(current), n);
+            else
+                hipLaunchKernelGGL((zpair_kernel<T, M, false>), dim3(grid),
+                                   dim3(256), 0, stream, static_cast<T*>(out),
+                                   static_cast<const T*>(earlier),
+                                   static_cast<const T*>(current), n);
             return hipGetLastError();
         });
     });

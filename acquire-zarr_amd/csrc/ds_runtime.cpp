@@ -5,10 +5,16 @@
 //   * the add_frame state machine (restates downsampler.cpp:306-401): level
 //     cascade, Z pairing against the stored earlier plane, odd-plane
 //     pass-through, emit-without-overwrite (:599-605);
-//   * take_frame (:403-414) served from pinned host buffers filled by async
-//     device->host copies queued behind the kernels.
+//   * take_frame (:403-414): the cached level frame is copied from HBM
+//     straight into the caller's buffer.
 // Runs of consecutive levels that only halve XY are fused into one cascade
 // launch (up to 4 levels per launch), so the frame is read from HBM once.
+//
+// Level buffers: every level L >= 1 owns two device slots.  A frame emitted
+// while the level's cache is empty becomes the cached frame (its slot is
+// then left alone until take_frame); new results always go to the other
+// slot, so an untaken frame is never overwritten — the reference's
+// unordered_map::emplace rule.
 #include "aqz_downsampler.h"
 #include "ds_kernels.hh"
 
@@ -20,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace {
@@ -67,6 +74,13 @@ halve(const aqz_dimension& d)
     return o;
 }
 
+bool
+env_flag(const char* name)
+{
+    const char* v = std::getenv(name);
+    return v && *v && std::strcmp(v, "0") != 0;
+}
+
 } // namespace
 
 struct aqz_ds
@@ -84,14 +98,14 @@ struct aqz_ds
     std::vector<uint8_t> has_partial;
 
     hipStream_t stream = nullptr;
-    void* d_in = nullptr;           // level-0 staging on device
-    std::vector<void*> d_level;     // level output buffers
-    std::vector<void*> d_partial;   // stored earlier plane (Z levels)
-    void* h_stage = nullptr;        // pinned level-0 staging
-    hipEvent_t stage_done = nullptr;
-    std::vector<void*> h_level;     // pinned take_frame cache
-    std::vector<uint8_t> cached;
-    std::vector<hipEvent_t> ready;
+    void* d_in = nullptr;                      // level-0 frame on device
+    std::vector<std::pair<void*, void*>> slot; // two output slots per level
+    std::vector<int> cached;                   // slot holding the untaken frame, -1 none
+    std::vector<void*> d_partial;              // stored earlier plane (Z levels)
+    hipEvent_t h2d_done = nullptr;
+    // optional pinned staging of host frames ($AQZ_PINNED_STAGING=1)
+    bool staged = false;
+    void* h_stage = nullptr;
     size_t device_bytes = 0;
     int last_batch_kind = -1;
 
@@ -107,6 +121,12 @@ struct aqz_ds
         err = what;
         return AQZ_INVALID_ARGUMENT;
     }
+    void* slot_ptr(uint32_t L, int k) const
+    {
+        return k == 0 ? slot[L].first : slot[L].second;
+    }
+    // where a new level-L frame is written: never the cached slot
+    void* out_slot(uint32_t L) const { return slot_ptr(L, cached[L] == 0 ? 1 : 0); }
 };
 
 namespace {
@@ -121,7 +141,7 @@ namespace {
 // Where the frames a level emits go.
 struct Sink
 {
-    // cache mode (add_frame): async D2H into the pinned take_frame slot
+    // false: streaming add_frame — the frame may become the cached one
     bool batch = false;
     // batch mode: frame k of level L goes to out[L] + k*bytes[L]
     void* const* out = nullptr;
@@ -134,32 +154,37 @@ elems(const aqz_ds* ds, uint32_t level)
     return uint64_t(ds->lv[level].width) * ds->lv[level].height;
 }
 
+// Working buffer for a level-L result: the caller's batch slot when the
+// sink is a batch, else the level's free device slot.
+void*
+level_target(aqz_ds* ds, uint32_t L, const Sink& sink)
+{
+    if (sink.batch)
+        return static_cast<uint8_t*>(sink.out[L]) +
+               (*sink.emitted)[L] * ds->bytes[L];
+    return ds->out_slot(L);
+}
+
 // emplace_downsampled_frame_ (downsampler.cpp:599-605).
 int
 emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink)
 {
     ++ds->count[level];
+    void* want = level_target(ds, level, sink);
+    if (want != d_frame) {
+        HIP_TRY(ds,
+                hipMemcpyAsync(want, d_frame, ds->bytes[level],
+                               hipMemcpyDeviceToDevice, ds->stream),
+                "hipMemcpyAsync D2D");
+    }
     if (sink.batch) {
-        auto& k = (*sink.emitted)[level];
-        uint8_t* dst = static_cast<uint8_t*>(sink.out[level]) + k * ds->bytes[level];
-        ++k;
-        if (dst != d_frame) {
-            HIP_TRY(ds,
-                    hipMemcpyAsync(dst, d_frame, ds->bytes[level],
-                                   hipMemcpyDeviceToDevice, ds->stream),
-                    "hipMemcpyAsync D2D");
-        }
+        ++(*sink.emitted)[level];
         return AQZ_OK;
     }
-    // unordered_map::emplace keeps an untaken frame; the new one is dropped.
-    if (ds->cached[level])
-        return AQZ_OK;
-    HIP_TRY(ds,
-            hipMemcpyAsync(ds->h_level[level], d_frame, ds->bytes[level],
-                           hipMemcpyDeviceToHost, ds->stream),
-            "hipMemcpyAsync D2H");
-    HIP_TRY(ds, hipEventRecord(ds->ready[level], ds->stream), "hipEventRecord");
-    ds->cached[level] = 1;
+    // unordered_map::emplace keeps an untaken frame; the new one is dropped
+    // (it stays in the free slot only as the next level's input).
+    if (ds->cached[level] < 0)
+        ds->cached[level] = (want == ds->slot[level].first) ? 0 : 1;
     return AQZ_OK;
 }
 
@@ -196,16 +221,9 @@ process_frame(aqz_ds* ds, const void* d_frame, const Sink& sink)
                    !ds->zh[L + k])
                 ++k;
             aqz::LevelOut outs[aqz::kMaxFusedLevels];
-            for (uint32_t j = 0; j < k; ++j) {
-                void* dst = ds->d_level[L + j];
-                if (sink.batch) {
-                    // write straight into the caller's batch slot
-                    dst = static_cast<uint8_t*>(sink.out[L + j]) +
-                          (*sink.emitted)[L + j] * ds->bytes[L + j];
-                }
-                outs[j] = { dst, elems(ds, L + j), ds->lv[L + j].width,
-                            ds->lv[L + j].height };
-            }
+            for (uint32_t j = 0; j < k; ++j)
+                outs[j] = { level_target(ds, L + j, sink), elems(ds, L + j),
+                            ds->lv[L + j].width, ds->lv[L + j].height };
             const aqz_level_desc& a = ds->lv[L - 1];
             if (aqz::cascade_supported(ds->dtype, cur, a.width, a.height, outs,
                                        int(k))) {
@@ -259,27 +277,28 @@ process_frame(aqz_ds* ds, const void* d_frame, const Sink& sink)
             break;
         }
 
+        void* target = level_target(ds, L, sink);
         const void* next = cur;
         if (ds->xy[L]) {
-            int rc = reduce_xy(ds, L, cur, ds->d_level[L]);
+            int rc = reduce_xy(ds, L, cur, target);
             if (rc)
                 return rc;
-            next = ds->d_level[L];
+            next = target;
         }
         if (average) {
             // average_two_frames(dst = earlier, src = current)
             HIP_TRY(ds,
-                    aqz::launch_zpair(ds->dtype, ds->method, ds->d_level[L],
+                    aqz::launch_zpair(ds->dtype, ds->method, target,
                                       ds->d_partial[L], next, elems(ds, L),
                                       ds->stream),
                     "zpair kernel");
             ds->has_partial[L] = 0;
-            next = ds->d_level[L];
+            next = target;
         }
         int rc = emit(ds, L, next, sink);
         if (rc)
             return rc;
-        cur = next;
+        cur = target; // emit() left the level's frame in `target`
         ++L;
     }
     return AQZ_OK;
@@ -302,18 +321,15 @@ release(aqz_ds* ds)
     if (ds->stream)
         (void)hipStreamSynchronize(ds->stream);
     (void)hipFree(ds->d_in);
-    for (void* p : ds->d_level)
-        (void)hipFree(p);
+    for (auto& s : ds->slot) {
+        (void)hipFree(s.first);
+        (void)hipFree(s.second);
+    }
     for (void* p : ds->d_partial)
         (void)hipFree(p);
     (void)hipHostFree(ds->h_stage);
-    for (void* p : ds->h_level)
-        (void)hipHostFree(p);
-    for (hipEvent_t e : ds->ready)
-        if (e)
-            (void)hipEventDestroy(e);
-    if (ds->stage_done)
-        (void)hipEventDestroy(ds->stage_done);
+    if (ds->h2d_done)
+        (void)hipEventDestroy(ds->h2d_done);
     if (ds->stream)
         (void)hipStreamDestroy(ds->stream);
     delete ds;
@@ -443,11 +459,10 @@ aqz_ds_create(const aqz_level_desc* levels,
     ds->zh.assign(n_levels, 0);
     ds->count.assign(n_levels, 0);
     ds->has_partial.assign(n_levels, 0);
-    ds->d_level.assign(n_levels, nullptr);
+    ds->slot.assign(n_levels, { nullptr, nullptr });
+    ds->cached.assign(n_levels, -1);
     ds->d_partial.assign(n_levels, nullptr);
-    ds->h_level.assign(n_levels, nullptr);
-    ds->cached.assign(n_levels, 0);
-    ds->ready.assign(n_levels, nullptr);
+    ds->staged = env_flag("AQZ_PINNED_STAGING");
     for (uint32_t l = 0; l < n_levels; ++l) {
         ds->bytes[l] = size_t(levels[l].width) * levels[l].height * ds->bpp;
         if (l > 0) {
@@ -469,26 +484,25 @@ aqz_ds_create(const aqz_level_desc* levels,
         return fail(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(e, "hipStreamCreate");
-    if ((e = hipEventCreateWithFlags(&ds->stage_done, hipEventDisableTiming)) != hipSuccess)
+    if ((e = hipEventCreateWithFlags(&ds->h2d_done, hipEventDisableTiming)) != hipSuccess)
         return fail(e, "hipEventCreate");
     if ((e = hipMalloc(&ds->d_in, ds->bytes[0])) != hipSuccess)
         return fail(e, "hipMalloc level 0");
-    if ((e = hipHostMalloc(&ds->h_stage, ds->bytes[0], hipHostMallocDefault)) != hipSuccess)
+    if (ds->staged &&
+        (e = hipHostMalloc(&ds->h_stage, ds->bytes[0], hipHostMallocDefault)) != hipSuccess)
         return fail(e, "hipHostMalloc staging");
     ds->device_bytes = ds->bytes[0];
     for (uint32_t l = 1; l < n_levels; ++l) {
-        if ((e = hipMalloc(&ds->d_level[l], ds->bytes[l])) != hipSuccess)
+        if ((e = hipMalloc(&ds->slot[l].first, ds->bytes[l])) != hipSuccess)
             return fail(e, "hipMalloc level");
-        ds->device_bytes += ds->bytes[l];
+        if ((e = hipMalloc(&ds->slot[l].second, ds->bytes[l])) != hipSuccess)
+            return fail(e, "hipMalloc level");
+        ds->device_bytes += 2 * ds->bytes[l];
         if (ds->zh[l]) {
             if ((e = hipMalloc(&ds->d_partial[l], ds->bytes[l])) != hipSuccess)
                 return fail(e, "hipMalloc partial");
             ds->device_bytes += ds->bytes[l];
         }
-        if ((e = hipHostMalloc(&ds->h_level[l], ds->bytes[l], hipHostMallocDefault)) != hipSuccess)
-            return fail(e, "hipHostMalloc level");
-        if ((e = hipEventCreateWithFlags(&ds->ready[l], hipEventDisableTiming)) != hipSuccess)
-            return fail(e, "hipEventCreate");
     }
     *out = ds;
     return AQZ_OK;
@@ -510,15 +524,27 @@ aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes)
                             " bytes, got " + std::to_string(nbytes));
     if (int rc = bind_device(ds))
         return rc;
-    // The staging buffer is free once the previous frame's upload finished.
-    HIP_TRY(ds, hipEventSynchronize(ds->stage_done), "hipEventSynchronize");
-    std::memcpy(ds->h_stage, host_frame, nbytes);
+    const void* src = host_frame;
+    if (ds->staged) {
+        // previous upload must be done before the staging buffer is reused
+        HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
+        std::memcpy(ds->h_stage, host_frame, nbytes);
+        src = ds->h_stage;
+    }
+    // Straight from the caller's (pageable) frame: the copy engine reads it
+    // at full PCIe rate, no host staging memcpy (tools/e2e_probe.cpp).
     HIP_TRY(ds,
-            hipMemcpyAsync(ds->d_in, ds->h_stage, nbytes, hipMemcpyHostToDevice,
-                           ds->stream),
+            hipMemcpyAsync(ds->d_in, src, nbytes, hipMemcpyHostToDevice, ds->stream),
             "hipMemcpyAsync H2D");
-    HIP_TRY(ds, hipEventRecord(ds->stage_done, ds->stream), "hipEventRecord");
-    return process_frame(ds, ds->d_in, Sink{});
+    HIP_TRY(ds, hipEventRecord(ds->h2d_done, ds->stream), "hipEventRecord");
+    int rc = process_frame(ds, ds->d_in, Sink{});
+    if (rc)
+        return rc;
+    if (!ds->staged) {
+        // the caller may reuse its frame as soon as we return
+        HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
+    }
+    return AQZ_OK;
 }
 
 int
@@ -548,7 +574,7 @@ aqz_ds_take_frame(aqz_ds* ds,
     *has_frame = 0;
     if (level == 0 || level >= ds->n)
         return AQZ_OK; // the reference's map lookup simply misses
-    if (!ds->cached[level])
+    if (ds->cached[level] < 0)
         return AQZ_OK;
     *has_frame = 1;
     if (nbytes)
@@ -559,9 +585,13 @@ aqz_ds_take_frame(aqz_ds* ds,
         return ds->fail_arg("take_frame: buffer too small");
     if (int rc = bind_device(ds))
         return rc;
-    HIP_TRY(ds, hipEventSynchronize(ds->ready[level]), "hipEventSynchronize");
-    std::memcpy(dst, ds->h_level[level], ds->bytes[level]);
-    ds->cached[level] = 0;
+    // HBM -> caller memory directly (stream-ordered after the kernels)
+    HIP_TRY(ds,
+            hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
+                           ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
+            "hipMemcpyAsync D2H");
+    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+    ds->cached[level] = -1;
     return AQZ_OK;
 }
 

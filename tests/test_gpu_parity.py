@@ -263,3 +263,28 @@ def test_full_size_properties(aqz):
         mid = res[1][L].view(torch.int16).view(n, h, w).to(torch.int32) & 0xFFFF
         hi = res[3][L].view(torch.int16).view(n, h, w).to(torch.int32) & 0xFFFF
         assert bool((lo <= mid).all()) and bool((mid <= hi).all())
+
+
+@pytest.mark.parametrize("staged", ["0", "1"])
+def test_host_staging_modes(aqz, oracle, monkeypatch, staged):
+    """add_frame uploads straight from the caller's pageable frame by default;
+    $AQZ_PINNED_STAGING=1 stages through pinned memory instead.  Both must
+    give the oracle's frames, including when the caller overwrites its buffer
+    right after add_frame returns and when levels are left untaken."""
+    monkeypatch.setenv("AQZ_PINNED_STAGING", staged)
+    rng = np.random.default_rng(77)
+    geo = [(96, 64, 6), (48, 32, 3), (24, 16, 2)]
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+    buf = np.empty((64, 96), np.uint16)
+    for i in range(12):
+        buf[:] = rng.integers(0, 65536, (64, 96), dtype=np.uint16)
+        ds.add_frame(buf)
+        ref.add_frame(buf.copy())
+        buf[:] = 0  # the caller reuses its frame immediately
+        levels = [1, 2] if i % 3 else [1]  # leave level 2 untaken sometimes
+        for L in levels:
+            a, b = ds.take_frame(L), ref.take_frame(L)
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert_parity(a, b, f"staged={staged} frame {i} L{L}")
