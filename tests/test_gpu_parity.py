@@ -288,3 +288,32 @@ def test_host_staging_modes(aqz, oracle, monkeypatch, staged):
             assert (a is None) == (b is None)
             if a is not None:
                 assert_parity(a, b, f"staged={staged} frame {i} L{L}")
+
+
+def test_reference_example_stream(aqz, oracle):
+    """BASELINE configs[0] as the reference ships it:
+    examples/stream-raw-multiscale-to-filesystem.c — 5-D t10 c8 z6/2 y48/16
+    x64/16 uint16, `downsampling_method` left zero-initialised (Decimate,
+    zarr.types.h:92), 10 frames of `i*1000 + j` (wrapping uint16).  Levels
+    z/y/x 6/48/64 -> 3/24/32 -> 2/12/16.  The GPU path
+    must reproduce the oracle frame for frame, readiness included."""
+    dims = [(aqz.TIME, 10, 5, 2), (aqz.CHANNEL, 8, 4, 2), (aqz.SPACE, 6, 2, 1),
+            (aqz.SPACE, 48, 16, 1), (aqz.SPACE, 64, 16, 2)]
+    levels = aqz.plan_levels(dims)
+    geo = aqz.level_geometry(levels)
+    assert geo == [(64, 48, 6), (32, 24, 3), (16, 12, 2)]
+    assert levels == oracle.plan_levels(dims)
+    for method in METHODS:  # the example's Decimate first, then the others
+        ds = aqz.Downsampler(geo, np.uint16, method)
+        ref = oracle.OracleDownsampler(geo, np.uint16, method)
+        j = np.arange(48 * 64, dtype=np.uint32)
+        for i in range(10):
+            frame = ((i * 1000 + j) & 0xFFFF).astype(np.uint16).reshape(48, 64)
+            ds.add_frame(frame)
+            ref.add_frame(frame)
+            for L in (1, 2):
+                a, b = ds.take_frame(L), ref.take_frame(L)
+                assert (a is None) == (b is None), f"m{method} frame {i} L{L}"
+                if a is not None:
+                    assert_parity(a, b, f"example m{method} frame {i} L{L}")
+        assert ds.take_frame(1) is None and ref.take_frame(1) is None

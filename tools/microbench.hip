@@ -45,6 +45,14 @@ fill_kernel(uint32_t* p, uint64_t n, uint32_t seed)
     }
 }
 
+__global__ void
+finite_kernel(uint32_t* p, uint64_t n)
+{
+    for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * blockDim.x)
+        p[i] &= ~(1u << 30);
+}
+
 __global__ __launch_bounds__(256) void
 read_kernel(const u32x4* p, uint64_t n, uint32_t* sink)
 {
@@ -202,6 +210,31 @@ cascade_pipelined(CascadeParams p)
     }
 }
 
+template<typename T, int C, bool NTS>
+__global__ __launch_bounds__(256) void
+cascade_t_variant(CascadeParams p)
+{
+    constexpr int NL = 4;
+    constexpr int R = 1 << NL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * 4;
+    for (uint32_t u = blockIdx.x * 4 + wib; u < p.total_units; u += nwaves) {
+        const uint32_t ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        const uint32_t uy = t % p.units_y;
+        const uint32_t f = t / p.units_y;
+        const uint32_t row0 = uy * R;
+        const uint32_t tile_col0 = ux * (64u * C);
+        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+        const bool interior = (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
+        if (interior)
+            cascade_unit<T, kMean, NL, C, true, false, NTS>(p, f, row0, col0, lane);
+        else
+            cascade_unit<T, kMean, NL, C, true, true, NTS>(p, f, row0, col0, lane);
+    }
+}
+
 __global__ void
 count_diff(const uint8_t* a, const uint8_t* b, uint64_t n, unsigned long long* bad)
 {
@@ -218,9 +251,125 @@ count_diff(const uint8_t* a, const uint8_t* b, uint64_t n, unsigned long long* b
 
 using namespace aqz;
 
+// f32 headline-shaped batch: product (4 floats per lane) vs 8 per lane.
+int
+run_f32(uint32_t B, int reps)
+{
+    const uint32_t W = 4096, H = 4096;
+    const uint64_t frame = uint64_t(W) * H;
+    const uint64_t in_bytes = frame * B * 4;
+    float* d_in;
+    CHECK(hipMalloc(&d_in, in_bytes));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0,
+                       reinterpret_cast<uint32_t*>(d_in), in_bytes / 4, 777u);
+    // keep the floats finite: clear the exponent's top bit (|x| < 2)
+    hipLaunchKernelGGL(finite_kernel, dim3(8192), dim3(256), 0, 0,
+                       reinterpret_cast<uint32_t*>(d_in), in_bytes / 4);
+    uint32_t w[4], h[4];
+    uint64_t lvl = 0;
+    for (int i = 0, ww = W, hh = H; i < 4; ++i) {
+        ww = (ww + 1) / 2;
+        hh = (hh + 1) / 2;
+        w[i] = ww;
+        h[i] = hh;
+        lvl += uint64_t(ww) * hh * 4;
+    }
+    const uint64_t alg = in_bytes + lvl * B;
+    std::vector<void*> ref(4), var(4);
+    for (int i = 0; i < 4; ++i) {
+        CHECK(hipMalloc(&ref[i], uint64_t(w[i]) * h[i] * 4 * B));
+        CHECK(hipMalloc(&var[i], uint64_t(w[i]) * h[i] * 4 * B));
+    }
+    auto params = [&](int C, std::vector<void*>& o) {
+        CascadeParams p{};
+        p.src = reinterpret_cast<const uint8_t*>(d_in);
+        p.src_frame_elems = frame;
+        p.W = W;
+        p.H = H;
+        p.units_x = (W + 64 * C - 1) / (64 * C);
+        p.units_y = (H + 15) / 16;
+        p.total_units = p.units_x * p.units_y * B;
+        for (int i = 0; i < 4; ++i) {
+            p.dst[i] = static_cast<uint8_t*>(o[i]);
+            p.dst_frame_elems[i] = uint64_t(w[i]) * h[i];
+            p.w[i] = w[i];
+            p.h[i] = h[i];
+        }
+        return p;
+    };
+    struct V
+    {
+        const char* name;
+        std::function<void()> run;
+        std::vector<float> us;
+    };
+    std::vector<V> vs;
+    vs.push_back({ "f32 product (C4 nt/nt)", [&] {
+                      LevelOut o[4];
+                      for (int i = 0; i < 4; ++i)
+                          o[i] = { ref[i], uint64_t(w[i]) * h[i], w[i], h[i] };
+                      CHECK(launch_cascade(8, 1, d_in, frame, W, H, o, 4, B, 0));
+                  }, {} });
+    vs.push_back({ "f32 C8 nt/nt", [&] {
+                      auto p = params(8, var);
+                      hipLaunchKernelGGL((cascade_t_variant<float, 8, true>),
+                                         dim3((p.total_units + 3) / 4), dim3(256), 0, 0, p);
+                  }, {} });
+    vs.push_back({ "f32 C8 nt/plain-store", [&] {
+                      auto p = params(8, var);
+                      hipLaunchKernelGGL((cascade_t_variant<float, 8, false>),
+                                         dim3((p.total_units + 3) / 4), dim3(256), 0, 0, p);
+                  }, {} });
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    for (auto& v : vs)
+        for (int i = 0; i < 2; ++i)
+            v.run();
+    CHECK(hipDeviceSynchronize());
+    for (int r = 0; r < 3; ++r)
+        for (auto& v : vs)
+            for (int i = 0; i < reps; ++i) {
+                CHECK(hipEventRecord(e0, 0));
+                v.run();
+                CHECK(hipEventRecord(e1, 0));
+                CHECK(hipEventSynchronize(e1));
+                float ms;
+                CHECK(hipEventElapsedTime(&ms, e0, e1));
+                v.us.push_back(ms * 1e3f);
+            }
+    unsigned long long* bad;
+    CHECK(hipMalloc(&bad, 8));
+    std::printf("f32 batch %u frames of %ux%u, alg bytes %.1f MB\n", B, W, H, alg / 1e6);
+    for (size_t k = 0; k < vs.size(); ++k) {
+        auto& v = vs[k];
+        std::sort(v.us.begin(), v.us.end());
+        const float med = v.us[v.us.size() / 2];
+        std::string verdict;
+        if (k > 0) {
+            v.run();
+            CHECK(hipMemset(bad, 0, 8));
+            for (int i = 0; i < 4; ++i)
+                hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, 0,
+                                   static_cast<uint8_t*>(var[i]),
+                                   static_cast<uint8_t*>(ref[i]),
+                                   uint64_t(w[i]) * h[i] * 4 * B, bad);
+            unsigned long long nb;
+            CHECK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
+            verdict = nb ? " MISMATCH" : " (== product)";
+        }
+        std::printf("%-26s median %9.1f us  min %9.1f us  %7.1f GB/s (%.1f%%)%s\n",
+                    v.name, med, v.us[0], alg / (med * 1e3),
+                    100.0 * alg / (med * 1e3) / 8000.0, verdict.c_str());
+    }
+    return 0;
+}
+
 int
 main(int argc, char** argv)
 {
+    if (argc > 3 && std::string(argv[3]) == "f32")
+        return run_f32(argc > 1 ? std::atoi(argv[1]) : 64, argc > 2 ? std::atoi(argv[2]) : 20);
     const uint32_t W = 4096, H = 4096, B = argc > 1 ? std::atoi(argv[1]) : 64;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 20;
     const int rounds = 3;
