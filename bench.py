@@ -84,6 +84,41 @@ def aggregate_gpix(world: int, frames_per_rank: int, W: int, H: int, steps: int,
     return world * frames_per_rank * W * H * steps / elapsed_max / 1e9
 
 
+def scatter_frames(pool, local, frame_bytes: int, frames_per_rank: int, dist,
+                   rank: int, world: int):
+    """Batched-frame config F over xGMI: rank 0 holds every rank's frames
+    contiguously in `pool` (rank r's block at r*frames_per_rank) and sends
+    each block to its rank with point-to-point ops (RCCL send/recv under
+    the nccl backend).  Returns the tensor this rank computes on."""
+    blk = frames_per_rank * frame_bytes
+    if rank == 0:
+        reqs = [dist.isend(pool[r * blk:(r + 1) * blk], dst=r) for r in range(1, world)]
+        for q in reqs:
+            q.wait()
+        return pool[:blk]
+    dist.irecv(local[:blk], src=0).wait()
+    return local[:blk]
+
+
+def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
+    """Send every rank's level outputs back to rank 0, which lays rank r's
+    block of level L at pool_levels[L][r*len:(r+1)*len] (rank 0's own block
+    is copied locally)."""
+    reqs = []
+    for L, buf in enumerate(level_bufs):
+        if buf is None:
+            continue
+        n = buf.numel()
+        if rank == 0:
+            pool_levels[L][:n].copy_(buf)
+            reqs += [dist.irecv(pool_levels[L][r * n:(r + 1) * n], src=r)
+                     for r in range(1, world)]
+        else:
+            reqs.append(dist.isend(buf, dst=0))
+    for q in reqs:
+        q.wait()
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -101,6 +136,10 @@ def parse():
                    help="skip the one-frame oracle spot check")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE traffic passes")
+    p.add_argument("--xgmi-scatter", action="store_true",
+                   help="N>1 only (BASELINE config F): every step, rank 0 scatters "
+                        "the ranks' frames over xGMI with RCCL p2p and gathers "
+                        "the levels back; timed end to end")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -162,9 +201,26 @@ def main():
     assert sptr, "need a non-null HIP stream"
 
     counts = [0] * n_levels
+    xgmi = args.xgmi_scatter and dist is not None
+    if xgmi:
+        # config F: rank 0's pool holds every rank's frames; levels return
+        # to rank 0.  Rank 0 computes on the first block of its pool.
+        if rank == 0:
+            pool = torch.empty(world * B * frame_bytes, dtype=torch.uint8, device="cuda")
+            for r in range(world):
+                pool[r * B * frame_bytes:(r + 1) * B * frame_bytes].copy_(d_in)
+            pool_levels = [None] + [torch.empty(world * o.numel(), dtype=torch.uint8,
+                                                device="cuda") for o in outs[1:]]
+        else:
+            pool, pool_levels = None, None
 
     def step():
-        counts[:] = ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
+        if xgmi:
+            mine = scatter_frames(pool, d_in, frame_bytes, B, dist, rank, world)
+            counts[:] = ds.run_device_batch(mine.data_ptr(), B, out_ptrs, sptr)
+            gather_levels(outs, pool_levels, dist, rank, world)
+        else:
+            counts[:] = ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
 
     if args.pmc_child:
         # launched under `rocprofv3 --pmc` by measure_traffic(): launches only
@@ -176,10 +232,11 @@ def main():
 
     # correctness spot check of one frame against the oracle (rank 0, N=1)
     check = None
+    if not args.no_check:
+        step()  # every rank: in --xgmi-scatter mode the step is collective
+        torch.cuda.synchronize()
     if not args.no_check and rank == 0:
         import oracle as orc_mod  # test infrastructure: checker only
-        step()
-        torch.cuda.synchronize()
         # first 2^(levels-1) frames (one aligned plane group for volumes)
         nchk = min(B, 1 << (n_levels - 1)) if Z else 1
         host = d_in[:nchk * frame_bytes].cpu().numpy().view(dtype).reshape(nchk, H, W)
@@ -275,7 +332,9 @@ def main():
                        "launches_per_step": launches,
                        "batch_path": {0: "per-frame", 1: "fused cascade",
                                       2: "fused volume"}.get(kind, "?"),
-                       "parallelism": f"frame-sharded x{world}, no collective",
+                       "parallelism": (f"rank-0 batch scattered/gathered over xGMI "
+                                       f"(RCCL p2p) x{world}" if xgmi else
+                                       f"frame-sharded x{world}, no collective"),
                        "check": check},
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,

@@ -65,3 +65,59 @@ def test_aggregate_counts_all_ranks():
     v8 = bench.aggregate_gpix(8, 64, 4096, 4096, 20, 0.01)
     assert v8 == pytest.approx(8 * v1)
     assert v1 == pytest.approx(64 * 4096 * 4096 * 20 / 0.01 / 1e9)
+
+
+def _scatter_worker(rank, world, port, q):
+    """Rank 0 owns all frames; scatter -> per-rank pyramid -> gather, on CPU
+    tensors over gloo.  The per-rank compute here is the oracle (test
+    infrastructure); on the GPU bench it is the HIP batch path."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import bench
+    import oracle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, H, W = 3, 24, 40
+    fb = H * W * 4
+    geo = [(40, 24, 1), (20, 12, 1), (10, 6, 1)]
+    rng = np.random.default_rng(5)
+    allf = rng.uniform(-1e3, 1e3, (world * B, H, W)).astype(np.float32)
+    pool = torch.from_numpy(allf.view(np.uint8).reshape(-1).copy()) if rank == 0 else None
+    local = torch.empty(B * fb, dtype=torch.uint8)
+    mine = bench.scatter_frames(pool, local, fb, B, dist, rank, world)
+    frames = mine.numpy().view(np.float32).reshape(B, H, W)
+    lv = [None]
+    for L in range(1, 3):
+        w, h, _ = geo[L]
+        outs = [oracle.cascade_2d(f, 3, 1)[L - 1] for f in frames]
+        lv.append(torch.from_numpy(np.stack(outs).view(np.uint8).reshape(-1).copy()))
+    pool_lv = [None] + [torch.empty(world * t.numel(), dtype=torch.uint8) for t in lv[1:]]
+    bench.gather_levels(lv, pool_lv, dist, rank, world)
+    if rank == 0:
+        ok = True
+        for L in range(1, 3):
+            w, h, _ = geo[L]
+            got = pool_lv[L].numpy().view(np.float32).reshape(world * B, h, w)
+            for i in range(world * B):
+                ok = ok and np.array_equal(got[i], oracle.cascade_2d(allf[i], 3, 1)[L - 1])
+        q.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_scatter_gather_logic():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok
