@@ -463,7 +463,9 @@ volume_level(const VolumeParams& p,
     }
 }
 
-template<typename T, int M, int NL, bool EDGE>
+// C = columns per lane (V = C*sizeof(T)/16 loads per row); ZFAST puts the
+// plane group innermost in the unit order.
+template<typename T, int M, int NL, int C, bool EDGE>
 __device__ __forceinline__ void
 volume_unit(const VolumeParams& p,
             uint32_t g,
@@ -471,9 +473,9 @@ volume_unit(const VolumeParams& p,
             uint32_t col0,
             int lane)
 {
-    constexpr int C = 16 / int(sizeof(T));
     constexpr int R = 1 << NL;
     constexpr int Z = 1 << NL;
+    constexpr int V = C * int(sizeof(T)) / 16;
     T v[Z][R][C];
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
@@ -481,48 +483,60 @@ volume_unit(const VolumeParams& p,
                        (uint64_t(g) * Z + z) * p.src_frame_elems;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            bool ok = true;
-            if constexpr (EDGE) {
-                ok = (row0 + r < p.H) && (col0 < p.W);
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const uint32_t col = col0 + uint32_t(k) * (16 / sizeof(T));
+                bool ok = true;
+                if constexpr (EDGE) {
+                    ok = (row0 + r < p.H) && (col < p.W);
+                }
+                u32x4 q = { 0u, 0u, 0u, 0u };
+                if (ok) {
+                    q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                      src + uint64_t(row0 + r) * p.W + col));
+                }
+                __builtin_memcpy(&v[z][r][k * (16 / sizeof(T))], &q, 16);
             }
-            u32x4 q = { 0u, 0u, 0u, 0u };
-            if (ok) {
-                q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-                  src + uint64_t(row0 + r) * p.W + col0));
-            }
-            __builtin_memcpy(&v[z][r][0], &q, 16);
         }
     }
     volume_level<T, M, C, 1, NL, Z, R, C, EDGE, true>(p, v, g, row0, col0, lane);
 }
 
-template<typename T, int M, int NL>
+template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool ZFAST = false>
 __global__ __launch_bounds__(256) void
 volume_kernel(VolumeParams p)
 {
-    constexpr int C = 16 / int(sizeof(T));
     constexpr int R = 1 << NL;
     const int lane = threadIdx.x & 63;
     const uint32_t wave_in_block =
       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t waves_per_block = blockDim.x >> 6;
     const uint32_t nwaves = gridDim.x * waves_per_block;
+    const uint32_t groups = p.total_units / (p.units_x * p.units_y);
     for (uint32_t u = blockIdx.x * waves_per_block + wave_in_block;
          u < p.total_units;
          u += nwaves) {
-        const uint32_t ux = u % p.units_x;
-        const uint32_t t = u / p.units_x;
-        const uint32_t uy = t % p.units_y;
-        const uint32_t g = t / p.units_y;
+        uint32_t ux, uy, g;
+        if constexpr (ZFAST) {
+            g = u % groups;
+            const uint32_t t = u / groups;
+            ux = t % p.units_x;
+            uy = t / p.units_x;
+        } else {
+            ux = u % p.units_x;
+            const uint32_t t = u / p.units_x;
+            uy = t % p.units_y;
+            g = t / p.units_y;
+        }
         const uint32_t row0 = uy * R;
         const uint32_t tile_col0 = ux * (64u * C);
         const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
         const bool interior =
           (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
         if (interior) {
-            volume_unit<T, M, NL, false>(p, g, row0, col0, lane);
+            volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
         } else {
-            volume_unit<T, M, NL, true>(p, g, row0, col0, lane);
+            volume_unit<T, M, NL, C, true>(p, g, row0, col0, lane);
         }
     }
 }

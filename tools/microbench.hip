@@ -365,9 +365,122 @@ run_f32(uint32_t B, int reps)
     return 0;
 }
 
+// volume (config V): 1024^2 x planes u16, 2 levels (XY+Z) per launch
+int
+run_volume(uint32_t planes, int reps)
+{
+    const uint32_t W = 1024, H = 1024;
+    const uint64_t frame = uint64_t(W) * H;
+    const uint64_t in_bytes = frame * planes * 2;
+    uint16_t* d_in;
+    CHECK(hipMalloc(&d_in, in_bytes));
+    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0,
+                       reinterpret_cast<uint32_t*>(d_in), in_bytes / 4, 99u);
+    const uint32_t w[2] = { 512, 256 }, h[2] = { 512, 256 };
+    const uint64_t alg = in_bytes + uint64_t(512) * 512 * 2 * (planes / 2) +
+                         uint64_t(256) * 256 * 2 * (planes / 4);
+    std::vector<void*> ref(2), var(2);
+    for (int i = 0; i < 2; ++i) {
+        CHECK(hipMalloc(&ref[i], uint64_t(w[i]) * h[i] * 2 * planes));
+        CHECK(hipMalloc(&var[i], uint64_t(w[i]) * h[i] * 2 * planes));
+    }
+    auto params = [&](int C, std::vector<void*>& o) {
+        VolumeParams p{};
+        p.src = reinterpret_cast<const uint8_t*>(d_in);
+        p.src_frame_elems = frame;
+        p.W = W;
+        p.H = H;
+        p.units_x = (W + 64 * C - 1) / (64 * C);
+        p.units_y = H / 4;
+        p.total_units = p.units_x * p.units_y * (planes / 4);
+        for (int i = 0; i < 2; ++i) {
+            p.dst[i] = static_cast<uint8_t*>(o[i]);
+            p.dst_frame_elems[i] = uint64_t(w[i]) * h[i];
+            p.w[i] = w[i];
+            p.h[i] = h[i];
+        }
+        return p;
+    };
+    struct V
+    {
+        const char* name;
+        std::function<void()> run;
+        std::vector<float> us;
+    };
+    std::vector<V> vs;
+    vs.push_back({ "volume product (C8)", [&] {
+                      LevelOut o[2];
+                      for (int i = 0; i < 2; ++i)
+                          o[i] = { ref[i], uint64_t(w[i]) * h[i], w[i], h[i] };
+                      CHECK(launch_volume(1, 1, d_in, frame, W, H, o, 2, planes, 0));
+                  }, {} });
+    auto add = [&](const char* name, auto kern, int C) {
+        vs.push_back({ name, [&, kern, C] {
+                          auto p = params(C, var);
+                          hipLaunchKernelGGL(kern, dim3((p.total_units + 3) / 4),
+                                             dim3(256), 0, 0, p);
+                      }, {} });
+    };
+    add("volume C16", volume_kernel<uint16_t, kMean, 2, 16, false>, 16);
+    add("volume C8 zfast", volume_kernel<uint16_t, kMean, 2, 8, true>, 8);
+    add("volume C16 zfast", volume_kernel<uint16_t, kMean, 2, 16, true>, 16);
+    vs.push_back({ "read (volume, nt)", [&] {
+                      hipLaunchKernelGGL(read_kernel, dim3(4096), dim3(256), 0, 0,
+                                         reinterpret_cast<const u32x4*>(d_in),
+                                         in_bytes / 16, reinterpret_cast<uint32_t*>(var[1]));
+                  }, {} });
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    for (auto& v : vs)
+        for (int i = 0; i < 2; ++i)
+            v.run();
+    CHECK(hipDeviceSynchronize());
+    for (int r = 0; r < 3; ++r)
+        for (auto& v : vs)
+            for (int i = 0; i < reps; ++i) {
+                CHECK(hipEventRecord(e0, 0));
+                v.run();
+                CHECK(hipEventRecord(e1, 0));
+                CHECK(hipEventSynchronize(e1));
+                float ms;
+                CHECK(hipEventElapsedTime(&ms, e0, e1));
+                v.us.push_back(ms * 1e3f);
+            }
+    unsigned long long* bad;
+    CHECK(hipMalloc(&bad, 8));
+    std::printf("volume 1024x1024x%u u16, alg bytes %.1f MB\n", planes, alg / 1e6);
+    for (size_t k = 0; k < vs.size(); ++k) {
+        auto& v = vs[k];
+        std::sort(v.us.begin(), v.us.end());
+        const float med = v.us[v.us.size() / 2];
+        std::string verdict;
+        const bool is_read = std::string(v.name).rfind("read", 0) == 0;
+        const uint64_t bytes = is_read ? in_bytes : alg;
+        if (k > 0 && !is_read) {
+            v.run();
+            CHECK(hipMemset(bad, 0, 8));
+            for (int i = 0; i < 2; ++i)
+                hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, 0,
+                                   static_cast<uint8_t*>(var[i]),
+                                   static_cast<uint8_t*>(ref[i]),
+                                   uint64_t(w[i]) * h[i] * 2 * (planes >> (i + 1)), bad);
+            unsigned long long nb;
+            CHECK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
+            verdict = nb ? " MISMATCH" : " (== product)";
+        }
+        std::printf("%-26s median %9.1f us  min %9.1f us  %7.1f GB/s (%.1f%%)%s\n",
+                    v.name, med, v.us[0], bytes / (med * 1e3),
+                    100.0 * bytes / (med * 1e3) / 8000.0, verdict.c_str());
+    }
+    return 0;
+}
+
 int
 main(int argc, char** argv)
 {
+    if (argc > 3 && std::string(argv[3]) == "vol")
+        return run_volume(argc > 1 ? std::atoi(argv[1]) : 256, argc > 2 ? std::atoi(argv[2]) : 20);
     if (argc > 3 && std::string(argv[3]) == "f32")
         return run_f32(argc > 1 ? std::atoi(argv[1]) : 64, argc > 2 ? std::atoi(argv[2]) : 20);
     const uint32_t W = 4096, H = 4096, B = argc > 1 ? std::atoi(argv[1]) : 64;
