@@ -33,7 +33,7 @@ METHODS = {"decimate": DECIMATE, "mean": MEAN, "min": MIN, "max": MAX}
 EXPORTS = (
     "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
-    "aqz_ds_last_batch_kind",
+    "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -86,6 +86,8 @@ def lib() -> ctypes.CDLL:
                                     ctypes.POINTER(i32)]
     L.aqz_ds_run_device_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
                                           ctypes.POINTER(u32), vp]
+    L.aqz_ds_run_host_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
+                                        ctypes.POINTER(u32)]
     L.aqz_ds_last_batch_kind.argtypes = [vp]
     L.aqz_ds_last_batch_kind.restype = i32
     L.aqz_ds_level_bytes.argtypes = [vp, u32]
@@ -198,6 +200,16 @@ class Downsampler:
 
     def level_bytes(self, level: int) -> int:
         return lib().aqz_ds_level_bytes(self._h, level)
+
+    def run_host_batch(self, host_frames: int, n_frames: int, host_outs):
+        """Pipelined host batch: `host_frames` and `host_outs[L]` are host
+        addresses (index 0 ignored).  Returns frames emitted per level."""
+        n = self.n_levels
+        outs = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in host_outs])
+        counts = (ctypes.c_uint32 * n)()
+        self._check(lib().aqz_ds_run_host_batch(self._h, host_frames, n_frames,
+                                                outs, counts))
+        return list(counts)
 
     def last_batch_kind(self) -> int:
         """0 per-frame, 1 fused 2-D cascade, 2 fused volume, -1 none."""

@@ -109,6 +109,16 @@ struct aqz_ds
     size_t device_bytes = 0;
     int last_batch_kind = -1;
 
+    // aqz_ds_run_host_batch pipeline, allocated on first use
+    struct Pipe
+    {
+        uint32_t group = 0;                  // frames per group
+        hipStream_t s_in = nullptr, s_work = nullptr, s_out = nullptr;
+        void* d_in[2] = { nullptr, nullptr };
+        std::vector<void*> d_out[2];         // per level, group-sized
+        hipEvent_t in_done[2] = {}, work_done[2] = {}, out_done[2] = {};
+    } pipe;
+
     std::string err;
 
     int fail(hipError_t e, const char* what)
@@ -330,6 +340,18 @@ release(aqz_ds* ds)
     (void)hipHostFree(ds->h_stage);
     if (ds->h2d_done)
         (void)hipEventDestroy(ds->h2d_done);
+    for (int b = 0; b < 2; ++b) {
+        (void)hipFree(ds->pipe.d_in[b]);
+        for (void* p : ds->pipe.d_out[b])
+            (void)hipFree(p);
+        for (hipEvent_t e : { ds->pipe.in_done[b], ds->pipe.work_done[b],
+                              ds->pipe.out_done[b] })
+            if (e)
+                (void)hipEventDestroy(e);
+    }
+    for (hipStream_t st : { ds->pipe.s_in, ds->pipe.s_work, ds->pipe.s_out })
+        if (st)
+            (void)hipStreamDestroy(st);
     if (ds->stream)
         (void)hipStreamDestroy(ds->stream);
     delete ds;
@@ -709,6 +731,128 @@ aqz_ds_run_device_batch(aqz_ds* ds,
     if (out_counts)
         std::copy(emitted.begin(), emitted.end(), out_counts);
     ds->stream = saved;
+    return rc;
+}
+
+namespace {
+
+// Frames per pipeline group: about 64 MiB of input per group, and a whole
+// number of plane groups when the pyramid pairs planes (so fused volume
+// launches see aligned groups).
+uint32_t
+pipe_group(const aqz_ds* ds, uint32_t n_frames)
+{
+    uint32_t g = uint32_t(std::max<size_t>(1, (size_t(64) << 20) / ds->bytes[0]));
+    uint32_t align = 1;
+    for (uint32_t l = 1; l < ds->n; ++l)
+        if (ds->zh[l])
+            align <<= 1;
+    g = std::max(align, (g / align) * align);
+    return std::min(g, std::max(align, n_frames));
+}
+
+int
+ensure_pipe(aqz_ds* ds, uint32_t group)
+{
+    auto& p = ds->pipe;
+    if (p.group >= group)
+        return AQZ_OK;
+    for (int b = 0; b < 2; ++b) {
+        (void)hipFree(p.d_in[b]);
+        p.d_in[b] = nullptr;
+        for (void* q : p.d_out[b])
+            (void)hipFree(q);
+        p.d_out[b].assign(ds->n, nullptr);
+    }
+    if (!p.s_in) {
+        HIP_TRY(ds, hipStreamCreateWithFlags(&p.s_in, hipStreamNonBlocking), "stream");
+        HIP_TRY(ds, hipStreamCreateWithFlags(&p.s_work, hipStreamNonBlocking), "stream");
+        HIP_TRY(ds, hipStreamCreateWithFlags(&p.s_out, hipStreamNonBlocking), "stream");
+        for (int b = 0; b < 2; ++b) {
+            HIP_TRY(ds, hipEventCreateWithFlags(&p.in_done[b], hipEventDisableTiming), "event");
+            HIP_TRY(ds, hipEventCreateWithFlags(&p.work_done[b], hipEventDisableTiming), "event");
+            HIP_TRY(ds, hipEventCreateWithFlags(&p.out_done[b], hipEventDisableTiming), "event");
+            // start "done" so the first waits pass
+            HIP_TRY(ds, hipEventRecord(p.work_done[b], p.s_work), "event");
+            HIP_TRY(ds, hipEventRecord(p.out_done[b], p.s_out), "event");
+        }
+    }
+    for (int b = 0; b < 2; ++b) {
+        HIP_TRY(ds, hipMalloc(&p.d_in[b], size_t(group) * ds->bytes[0]), "hipMalloc pipe");
+        for (uint32_t l = 1; l < ds->n; ++l)
+            HIP_TRY(ds, hipMalloc(&p.d_out[b][l], size_t(group) * ds->bytes[l]),
+                    "hipMalloc pipe");
+    }
+    p.group = group;
+    return AQZ_OK;
+}
+
+} // namespace
+
+int
+aqz_ds_run_host_batch(aqz_ds* ds,
+                      const void* host_frames,
+                      uint32_t n_frames,
+                      void* const* host_out_levels,
+                      uint32_t* out_counts)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (!host_frames || !host_out_levels)
+        return ds->fail_arg("run_host_batch: null buffer");
+    for (uint32_t l = 1; l < ds->n; ++l)
+        if (!host_out_levels[l])
+            return ds->fail_arg("run_host_batch: null output for level " +
+                                std::to_string(l));
+    if (int rc = bind_device(ds))
+        return rc;
+    const uint32_t group = pipe_group(ds, n_frames);
+    if (int rc = ensure_pipe(ds, group))
+        return rc;
+    auto& p = ds->pipe;
+    std::vector<uint32_t> total(ds->n, 0);
+    const uint8_t* src = static_cast<const uint8_t*>(host_frames);
+    int rc = AQZ_OK;
+    uint32_t k = 0;
+    for (uint32_t f0 = 0; f0 < n_frames && rc == AQZ_OK; f0 += group, ++k) {
+        const int b = int(k & 1);
+        const uint32_t g = std::min(group, n_frames - f0);
+        // upload: buffer b is free once group k-2's kernels are done with it
+        HIP_TRY(ds, hipStreamWaitEvent(p.s_in, p.work_done[b], 0), "wait");
+        HIP_TRY(ds,
+                hipMemcpyAsync(p.d_in[b], src + size_t(f0) * ds->bytes[0],
+                               size_t(g) * ds->bytes[0], hipMemcpyHostToDevice,
+                               p.s_in),
+                "hipMemcpyAsync H2D");
+        HIP_TRY(ds, hipEventRecord(p.in_done[b], p.s_in), "event");
+        // kernels: after the upload, and after group k-2's download of d_out[b]
+        HIP_TRY(ds, hipStreamWaitEvent(p.s_work, p.in_done[b], 0), "wait");
+        HIP_TRY(ds, hipStreamWaitEvent(p.s_work, p.out_done[b], 0), "wait");
+        std::vector<uint32_t> counts(ds->n, 0);
+        rc = aqz_ds_run_device_batch(ds, p.d_in[b], g, p.d_out[b].data(),
+                                     counts.data(), p.s_work);
+        if (rc)
+            break;
+        HIP_TRY(ds, hipEventRecord(p.work_done[b], p.s_work), "event");
+        // download every frame this group emitted, appended per level
+        HIP_TRY(ds, hipStreamWaitEvent(p.s_out, p.work_done[b], 0), "wait");
+        for (uint32_t l = 1; l < ds->n; ++l) {
+            if (!counts[l])
+                continue;
+            uint8_t* dst = static_cast<uint8_t*>(host_out_levels[l]) +
+                           size_t(total[l]) * ds->bytes[l];
+            HIP_TRY(ds,
+                    hipMemcpyAsync(dst, p.d_out[b][l], size_t(counts[l]) * ds->bytes[l],
+                                   hipMemcpyDeviceToHost, p.s_out),
+                    "hipMemcpyAsync D2H");
+            total[l] += counts[l];
+        }
+        HIP_TRY(ds, hipEventRecord(p.out_done[b], p.s_out), "event");
+    }
+    HIP_TRY(ds, hipStreamSynchronize(p.s_out), "hipStreamSynchronize");
+    total[0] = n_frames;
+    if (out_counts)
+        std::copy(total.begin(), total.end(), out_counts);
     return rc;
 }
 

@@ -307,6 +307,8 @@ def main():
             cpu_baseline = measure_cpu(geo, dtype, method, args.cpu_seconds, list(frames))
         if args.e2e_frames > 0:
             e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device)
+            e2e["pipelined"] = measure_e2e_pipelined(aqz, torch, geo, dtype, method,
+                                                     d_in, min(B, 64), device)
 
     if rank == 0:
         metric = HEADLINE_METRIC if args.workload == "4096x4096_u16" else (
@@ -453,6 +455,34 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device):
             "ms_per_frame": round(el / n_frames * 1e3, 3),
             "path": "add_frame(host) + take_frame(all levels), synchronous, 1 GPU",
             "frames": n_frames}
+
+
+def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device):
+    """Host-resident frames through aqz_ds_run_host_batch: pinned input and
+    level buffers, upload / kernels / download overlapped in double-buffered
+    groups — the PCIe-inclusive rate a caller that overlaps frames gets."""
+    W, H, _ = geo[0]
+    bpp = np.dtype(dtype).itemsize
+    src = d_in[:n * W * H * bpp].cpu().pin_memory()
+    outs = [None] + [torch.empty(n * w * h * bpp, dtype=torch.uint8).pin_memory()
+                     for w, h, _ in geo[1:]]
+    ptrs = [0] + [o.data_ptr() for o in outs[1:]]
+    ds = aqz.Downsampler(geo, dtype, method, device=device)
+    ds.run_host_batch(src.data_ptr(), n, ptrs)  # warm: allocates the pipeline
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ds.run_host_batch(src.data_ptr(), n, ptrs)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    ds.close()
+    in_bytes = n * W * H * bpp
+    out_bytes = sum(o.numel() for o in outs[1:])
+    return {"value": round(n * W * H / best / 1e9, 3), "unit": "GPixels/s",
+            "ms_per_frame": round(best / n * 1e3, 3),
+            "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 1),
+            "path": "aqz_ds_run_host_batch, pinned host in/out, "
+                    f"{n} frames, H2D/kernels/D2H overlapped"}
 
 
 if __name__ == "__main__":

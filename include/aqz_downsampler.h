@@ -195,6 +195,23 @@ int aqz_ds_run_device_batch(aqz_ds* ds,
                             void* hip_stream);
 
 /*
+ * Host-resident batch, pipelined (overlapping frames).
+ * Same results as aqz_ds_add_frame + aqz_ds_take_frame(every level) on each
+ * of `n_frames` consecutive frames of `host_frames`: the k-th frame emitted at
+ * level L is written to `host_out_levels[L] + k * level_bytes(L)`
+ * (`host_out_levels[0]` ignored; `out_counts` optional, n_levels entries).
+ * Frames move in double-buffered groups on three streams — upload, kernels,
+ * download — so both PCIe directions and the kernels overlap.  Pass pinned
+ * (hipHostMalloc'd or registered) buffers for full overlap; pageable memory
+ * works but serialises the copies.  Blocks until every level is on the host.
+ */
+int aqz_ds_run_host_batch(aqz_ds* ds,
+                          const void* host_frames,
+                          uint32_t n_frames,
+                          void* const* host_out_levels,
+                          uint32_t* out_counts);
+
+/*
  * Diagnostic: the path the last aqz_ds_run_device_batch took —
  * 0 = per-frame state machine, 1 = fused 2-D cascade, 2 = fused volume
  * (XY + Z), -1 = none yet.

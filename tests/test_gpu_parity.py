@@ -317,3 +317,44 @@ def test_reference_example_stream(aqz, oracle):
                 if a is not None:
                     assert_parity(a, b, f"example m{method} frame {i} L{L}")
         assert ds.take_frame(1) is None and ref.take_frame(1) is None
+
+
+@pytest.mark.parametrize("geo_kind", ["2d", "3d_odd_stack", "3d_fused", "2d_generic"])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_batch_pipeline(aqz, oracle, geo_kind, pinned):
+    """aqz_ds_run_host_batch: double-buffered groups over three streams must
+    equal add_frame + take_frame on every frame (oracle stream), with group
+    boundaries landing mid-stack and a ragged last group."""
+    torch = torch_cuda()
+    geo, _, _ = BATCH_GEOMETRIES[geo_kind]
+    w, h, _ = geo[0]
+    n = 37 if geo_kind != "3d_fused" else 40
+    rng = np.random.default_rng(seed_of("host_batch", geo_kind))
+    frames = random_frames(rng, np.uint16, (n, h, w))
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+    expected = {L: [] for L in range(1, len(geo))}
+    for f in frames:
+        ref.add_frame(f)
+        for L in expected:
+            r = ref.take_frame(L)
+            if r is not None:
+                expected[L].append(r)
+    if pinned:
+        src = torch.from_numpy(frames.view(np.uint8).reshape(-1).copy()).pin_memory()
+        outs = [None] + [torch.empty(n * gw * gh * 2, dtype=torch.uint8).pin_memory()
+                         for gw, gh, _ in geo[1:]]
+        src_ptr = src.data_ptr()
+        out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
+        views = [None] + [o.numpy() for o in outs[1:]]
+    else:
+        src_ptr = frames.ctypes.data
+        views = [None] + [np.empty(n * gw * gh * 2, np.uint8) for gw, gh, _ in geo[1:]]
+        out_ptrs = [0] + [v.ctypes.data for v in views[1:]]
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    counts = ds.run_host_batch(src_ptr, n, out_ptrs)
+    for L in expected:
+        gw, gh, _ = geo[L]
+        assert counts[L] == len(expected[L])
+        got = views[L].view(np.uint16).reshape(n, gh, gw)
+        for k, e in enumerate(expected[L]):
+            assert_parity(got[k], e, f"host batch {geo_kind} L{L} frame {k}")
