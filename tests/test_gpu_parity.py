@@ -358,3 +358,50 @@ def test_host_batch_pipeline(aqz, oracle, geo_kind, pinned):
         got = views[L].view(np.uint16).reshape(n, gh, gw)
         for k, e in enumerate(expected[L]):
             assert_parity(got[k], e, f"host batch {geo_kind} L{L} frame {k}")
+
+
+FULL_CONFIGS = {
+    # BASELINE.json configs at full size: (geometry, dtype, frames)
+    "c1_512_u8": (halving_geometry(512, 512, 3), np.uint8, 4),
+    "c2_2048_u16": (halving_geometry(2048, 2048, 4), np.uint16, 4),
+    "c3_4096_f32": (halving_geometry(4096, 4096, 5), np.float32, 2),
+    "c4_volume_1024x256_u16": ([(1024, 1024, 256), (512, 512, 128), (256, 256, 64)],
+                               np.uint16, 256),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FULL_CONFIGS))
+@pytest.mark.parametrize("method", METHODS)
+def test_full_size_configs_vs_oracle(aqz, oracle, name, method):
+    """Every BASELINE config at its full size through the device batch path
+    (the benchmarked kernels), checked frame by frame against the oracle;
+    the volume is one whole 1024x1024x256 stack."""
+    torch = torch_cuda()
+    geo, dtype, n = FULL_CONFIGS[name]
+    w, h, _ = geo[0]
+    rng = np.random.default_rng(seed_of("full", name, method))
+    if np.dtype(dtype).kind == "f":
+        frames = rng.uniform(-1e3, 1e3, (n, h, w)).astype(dtype)
+    else:
+        frames = rng.integers(0, np.iinfo(dtype).max, (n, h, w), dtype=dtype,
+                              endpoint=True)
+    bpp = np.dtype(dtype).itemsize
+    d_in = to_device(frames)
+    outs = [None] + [empty_device(n * gw * gh * bpp) for gw, gh, _ in geo[1:]]
+    ds = aqz.Downsampler(geo, dtype, method)
+    counts = ds.run_device_batch(d_in.data_ptr(), n, [0] + [o.data_ptr() for o in outs[1:]],
+                                 launch_stream())
+    torch.cuda.synchronize()
+    assert ds.last_batch_kind() in (1, 2)
+    ref = oracle.OracleDownsampler(geo, dtype, method)
+    got = {L: from_device(outs[L], dtype, (n, geo[L][1], geo[L][0]))
+           for L in range(1, len(geo))}
+    k = {L: 0 for L in got}
+    for i in range(n):
+        ref.add_frame(frames[i])
+        for L in got:
+            r = ref.take_frame(L)
+            if r is not None:
+                assert_parity(got[L][k[L]], r, f"{name} m{method} L{L} #{k[L]}")
+                k[L] += 1
+    assert [k[L] for L in got] == [counts[L] for L in got]
