@@ -33,7 +33,8 @@ METHODS = {"decimate": DECIMATE, "mean": MEAN, "min": MIN, "max": MAX}
 EXPORTS = (
     "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
-    "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch",
+    "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
+    "aqz_tile_frame_device",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -86,6 +87,9 @@ def lib() -> ctypes.CDLL:
                                     ctypes.POINTER(i32)]
     L.aqz_ds_run_device_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
                                           ctypes.POINTER(u32), vp]
+    L.aqz_ds_take_frame_tiled.argtypes = [vp, u32, u32, u32, vp, sz, vp,
+                                          ctypes.POINTER(sz), ctypes.POINTER(i32)]
+    L.aqz_tile_frame_device.argtypes = [i32, vp, u32, u32, u32, u32, vp, vp, vp]
     L.aqz_ds_run_host_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
                                         ctypes.POINTER(u32)]
     L.aqz_ds_last_batch_kind.argtypes = [vp]
@@ -201,6 +205,21 @@ class Downsampler:
     def level_bytes(self, level: int) -> int:
         return lib().aqz_ds_level_bytes(self._h, level)
 
+    def take_frame_tiled(self, level: int, tile_rows: int, tile_cols: int):
+        """Chunk-tiled take: (tiles[n_tiles, tile_rows, tile_cols],
+        nonzero[n_tiles] bool) or None."""
+        if not 0 <= level < self.n_levels:
+            return None
+        w, h, _ = self.geometry[level]
+        nt = (-(-h // tile_rows)) * (-(-w // tile_cols))
+        out = np.empty((nt, tile_rows, tile_cols), dtype=self.dtype)
+        nz = np.empty(nt, dtype=np.uint8)
+        nb, has = ctypes.c_size_t(0), ctypes.c_int(0)
+        self._check(lib().aqz_ds_take_frame_tiled(
+            self._h, level, tile_rows, tile_cols, out.ctypes.data, out.nbytes,
+            nz.ctypes.data, ctypes.byref(nb), ctypes.byref(has)))
+        return (out, nz.astype(bool)) if has.value else None
+
     def run_host_batch(self, host_frames: int, n_frames: int, host_outs):
         """Pipelined host batch: `host_frames` and `host_outs[L]` are host
         addresses (index 0 ignored).  Returns frames emitted per level."""
@@ -249,6 +268,18 @@ class Downsampler:
             self._h, device_frames, n_frames, outs, counts,
             ctypes.c_void_p(stream) if stream else None))
         return list(counts)
+
+
+def tile_frame_device(dtype, device_frame: int, width: int, height: int,
+                      tile_rows: int, tile_cols: int, device_tiles: int,
+                      device_nonzero: int, stream: int = 0):
+    """aqz_tile_frame_device (asynchronous on `stream`)."""
+    L = lib()
+    rc = L.aqz_tile_frame_device(dtype_code(dtype), device_frame, width, height,
+                                 tile_rows, tile_cols, device_tiles, device_nonzero,
+                                 ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
 
 
 def alg_bytes_per_frame(geometry, bpp: int) -> int:

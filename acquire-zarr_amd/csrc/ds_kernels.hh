@@ -101,6 +101,20 @@ hipError_t launch_zpair(int dtype,
                         uint64_t n,
                         hipStream_t stream);
 
+// Chunk tiling of one W x H frame (array.cpp:507-622 / chunk.cpp:17-58):
+// `dst` receives n_tiles x tile_rows x tile_cols elements, tile-major,
+// zero-padded; `nonzero[t]` (device, one u32 per tile, cleared here) is set
+// when tile t holds any nonzero byte.
+hipError_t launch_tile_frame(int dtype,
+                             const void* src,
+                             uint32_t W,
+                             uint32_t H,
+                             uint32_t tile_rows,
+                             uint32_t tile_cols,
+                             void* dst,
+                             uint32_t* nonzero,
+                             hipStream_t stream);
+
 // Tuning knob for the cascade grid (waves resident per CU × CUs); 0 = auto.
 void set_cascade_grid_cap(uint32_t blocks);
 

@@ -608,6 +608,68 @@ zpair_kernel(T* out, const T* earlier, const T* current, uint64_t n)
     }
 }
 
+// ---- chunk tiling --------------------------------------
+//
+// Array::write_frame_to_chunks_ (array.cpp:507-622) copies each frame tile's
+// rows into its chunk buffer at stride tile_cols*bpp (Chunk::write_tile_rows,
+// chunk.cpp:17-58), leaving the overhang zero, and byte-scans the copied rows
+// for the all-zero-chunk skip.  This kernel emits the frame already in that
+// tile order (zero-padded) plus the scan result, so the host does one
+// contiguous copy per tile and no scan.  Grid: `slices` blocks per tile, one
+// block-wide OR per block.
+
+template<typename T>
+__device__ __forceinline__ bool
+nonzero_bits(T v)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t b;
+        __builtin_memcpy(&b, &v, 8);
+        return b != 0;
+    } else {
+        uint32_t b = 0;
+        __builtin_memcpy(&b, &v, sizeof(T));
+        return b != 0;
+    }
+}
+
+template<typename T>
+__global__ __launch_bounds__(256) void
+tile_kernel(const T* __restrict__ src,
+            uint32_t W,
+            uint32_t H,
+            uint32_t tile_rows,
+            uint32_t tile_cols,
+            uint32_t n_tiles_x,
+            uint32_t slices,
+            T* __restrict__ dst,
+            uint32_t* __restrict__ nonzero)
+{
+    const uint32_t t = blockIdx.x / slices;
+    const uint32_t s = blockIdx.x % slices;
+    const uint32_t ty = t / n_tiles_x, tx = t % n_tiles_x;
+    const uint64_t tile_elems = uint64_t(tile_rows) * tile_cols;
+    const uint64_t per = (tile_elems + slices - 1) / slices;
+    const uint64_t e0 = uint64_t(s) * per;
+    const uint64_t e1 = e0 + per < tile_elems ? e0 + per : tile_elems;
+    T* out = dst + uint64_t(t) * tile_elems;
+    bool any = false;
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const uint32_t r = uint32_t(e / tile_cols);
+        const uint32_t c = uint32_t(e % tile_cols);
+        const uint32_t row = ty * tile_rows + r;
+        const uint32_t col = tx * tile_cols + c;
+        T v = T(0);
+        if (row < H && col < W) {
+            v = src[uint64_t(row) * W + col];
+            any = any || nonzero_bits(v);
+        }
+        out[e] = v;
+    }
+    if (__syncthreads_or(any) && threadIdx.x == 0)
+        atomicOr(nonzero + t, 1u);
+}
+
 // ---- dispatch ---------------------------------------------------------------
 
 template<typename F>
@@ -874,6 +936,40 @@ launch_volume(int dtype,
                                    dim3(256), 0, stream, p);
             return hipGetLastError();
         });
+    });
+}
+
+hipError_t
+launch_tile_frame(int dtype,
+                  const void* src,
+                  uint32_t W,
+                  uint32_t H,
+                  uint32_t tile_rows,
+                  uint32_t tile_cols,
+                  void* dst,
+                  uint32_t* nonzero,
+                  hipStream_t stream)
+{
+    if (W == 0 || H == 0 || tile_rows == 0 || tile_cols == 0)
+        return hipErrorInvalidValue;
+    const uint32_t ntx = (W + tile_cols - 1) / tile_cols;
+    const uint32_t nty = (H + tile_rows - 1) / tile_rows;
+    const uint64_t tile_elems = uint64_t(tile_rows) * tile_cols;
+    // ~8 K elements per block, at most 64 blocks per tile
+    const uint32_t slices =
+      uint32_t(std::min<uint64_t>(64, std::max<uint64_t>(1, tile_elems / 8192)));
+    const uint64_t blocks = uint64_t(ntx) * nty * slices;
+    if (blocks >= (1ull << 31))
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(nonzero, 0, sizeof(uint32_t) * ntx * nty, stream);
+    if (e != hipSuccess)
+        return e;
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((tile_kernel<T>), dim3(uint32_t(blocks)), dim3(256), 0,
+                           stream, static_cast<const T*>(src), W, H, tile_rows,
+                           tile_cols, ntx, slices, static_cast<T*>(dst), nonzero);
+        return hipGetLastError();
     });
 }
 

@@ -109,6 +109,12 @@ struct aqz_ds
     size_t device_bytes = 0;
     int last_batch_kind = -1;
 
+    // aqz_ds_take_frame_tiled scratch, grown on demand
+    void* d_tiles = nullptr;
+    size_t d_tiles_bytes = 0;
+    uint32_t* d_nonzero = nullptr;
+    size_t d_nonzero_n = 0;
+
     // aqz_ds_run_host_batch pipeline, allocated on first use
     struct Pipe
     {
@@ -338,6 +344,8 @@ release(aqz_ds* ds)
     for (void* p : ds->d_partial)
         (void)hipFree(p);
     (void)hipHostFree(ds->h_stage);
+    (void)hipFree(ds->d_tiles);
+    (void)hipFree(ds->d_nonzero);
     if (ds->h2d_done)
         (void)hipEventDestroy(ds->h2d_done);
     for (int b = 0; b < 2; ++b) {
@@ -614,6 +622,99 @@ aqz_ds_take_frame(aqz_ds* ds,
             "hipMemcpyAsync D2H");
     HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
     ds->cached[level] = -1;
+    return AQZ_OK;
+}
+
+int
+aqz_ds_take_frame_tiled(aqz_ds* ds,
+                        uint32_t level,
+                        uint32_t tile_rows,
+                        uint32_t tile_cols,
+                        void* dst,
+                        size_t cap,
+                        uint8_t* tile_nonzero,
+                        size_t* nbytes,
+                        int* has_frame)
+{
+    if (!ds || !has_frame)
+        return AQZ_INVALID_ARGUMENT;
+    *has_frame = 0;
+    if (tile_rows == 0 || tile_cols == 0)
+        return ds->fail_arg("take_frame_tiled: empty tile");
+    if (level == 0 || level >= ds->n || ds->cached[level] < 0)
+        return AQZ_OK;
+    const aqz_level_desc& lv = ds->lv[level];
+    const size_t ntx = (lv.width + tile_cols - 1) / tile_cols;
+    const size_t nty = (lv.height + tile_rows - 1) / tile_rows;
+    const size_t bytes = ntx * nty * tile_rows * tile_cols * ds->bpp;
+    *has_frame = 1;
+    if (nbytes)
+        *nbytes = bytes;
+    if (!dst)
+        return AQZ_OK;
+    if (cap < bytes)
+        return ds->fail_arg("take_frame_tiled: buffer too small");
+    if (int rc = bind_device(ds))
+        return rc;
+    if (ds->d_tiles_bytes < bytes) {
+        (void)hipFree(ds->d_tiles);
+        ds->d_tiles = nullptr;
+        ds->d_tiles_bytes = 0;
+        HIP_TRY(ds, hipMalloc(&ds->d_tiles, bytes), "hipMalloc tiles");
+        ds->d_tiles_bytes = bytes;
+    }
+    if (ds->d_nonzero_n < ntx * nty) {
+        (void)hipFree(ds->d_nonzero);
+        ds->d_nonzero = nullptr;
+        ds->d_nonzero_n = 0;
+        HIP_TRY(ds, hipMalloc(&ds->d_nonzero, sizeof(uint32_t) * ntx * nty),
+                "hipMalloc tile flags");
+        ds->d_nonzero_n = ntx * nty;
+    }
+    HIP_TRY(ds,
+            aqz::launch_tile_frame(ds->dtype, ds->slot_ptr(level, ds->cached[level]),
+                                   lv.width, lv.height, tile_rows, tile_cols,
+                                   ds->d_tiles, ds->d_nonzero, ds->stream),
+            "tile kernel");
+    HIP_TRY(ds,
+            hipMemcpyAsync(dst, ds->d_tiles, bytes, hipMemcpyDeviceToHost, ds->stream),
+            "hipMemcpyAsync D2H");
+    std::vector<uint32_t> flags(ntx * nty);
+    HIP_TRY(ds,
+            hipMemcpyAsync(flags.data(), ds->d_nonzero, sizeof(uint32_t) * flags.size(),
+                           hipMemcpyDeviceToHost, ds->stream),
+            "hipMemcpyAsync D2H");
+    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+    if (tile_nonzero)
+        for (size_t t = 0; t < flags.size(); ++t)
+            tile_nonzero[t] = flags[t] ? 1 : 0;
+    ds->cached[level] = -1;
+    return AQZ_OK;
+}
+
+int
+aqz_tile_frame_device(int dtype,
+                      const void* device_frame,
+                      uint32_t width,
+                      uint32_t height,
+                      uint32_t tile_rows,
+                      uint32_t tile_cols,
+                      void* device_tiles,
+                      uint32_t* device_nonzero,
+                      void* hip_stream)
+{
+    if (!aqz::dtype_valid(dtype) || !device_frame || !device_tiles ||
+        !device_nonzero) {
+        set_global_error("tile_frame_device: invalid argument");
+        return AQZ_INVALID_ARGUMENT;
+    }
+    const hipError_t e = aqz::launch_tile_frame(
+      dtype, device_frame, width, height, tile_rows, tile_cols, device_tiles,
+      device_nonzero, static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) {
+        set_global_error("tile_frame_device: %s", hipGetErrorString(e));
+        return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
+    }
     return AQZ_OK;
 }
 

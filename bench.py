@@ -306,7 +306,8 @@ def main():
             frames = d_in[:nf * frame_bytes].cpu().numpy().view(dtype).reshape(nf, H, W)
             cpu_baseline = measure_cpu(geo, dtype, method, args.cpu_seconds, list(frames))
         if args.e2e_frames > 0:
-            e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device)
+            e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device,
+                              tile=(chunk, chunk))
             e2e["pipelined"] = measure_e2e_pipelined(aqz, torch, geo, dtype, method,
                                                      d_in, min(B, 64), device)
 
@@ -429,7 +430,7 @@ def measure_cpu(geo, dtype, method, seconds, frames):
             "ms_per_frame": round(el / n * 1e3, 3)}
 
 
-def measure_e2e(aqz, geo, dtype, method, n_frames, device):
+def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
     """Streaming drop-in path: pageable host frame -> pinned staging -> H2D ->
     fused kernels -> D2H of levels 1..N -> take_frame copies."""
     W, H, _ = geo[0]
@@ -450,11 +451,23 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device):
         for L in range(1, len(geo)):
             ds.take_frame(L)
     el = time.perf_counter() - t0
+    res = {"value": round(n_frames * W * H / el / 1e9, 3), "unit": "GPixels/s",
+           "ms_per_frame": round(el / n_frames * 1e3, 3),
+           "path": "add_frame(host) + take_frame(all levels), synchronous, 1 GPU",
+           "frames": n_frames}
+    if tile:
+        # same loop with the chunk-tiled take: levels
+        # arrive tile-major with the zero scan done on the GPU
+        t0 = time.perf_counter()
+        for i in range(n_frames):
+            ds.add_frame(frames[i % 4])
+            for L in range(1, len(geo)):
+                ds.take_frame_tiled(L, tile[0], tile[1])
+        el = time.perf_counter() - t0
+        res["tiled_take_ms_per_frame"] = round(el / n_frames * 1e3, 3)
+        res["tile"] = list(tile)
     ds.close()
-    return {"value": round(n_frames * W * H / el / 1e9, 3), "unit": "GPixels/s",
-            "ms_per_frame": round(el / n_frames * 1e3, 3),
-            "path": "add_frame(host) + take_frame(all levels), synchronous, 1 GPU",
-            "frames": n_frames}
+    return res
 
 
 def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device):

@@ -177,6 +177,44 @@ int aqz_ds_take_frame(aqz_ds* ds,
                       int* has_frame);
 
 /*
+ * Chunk-tiled take.  Same as aqz_ds_take_frame, but the
+ * frame arrives in the tile order Array::write_frame_to_chunks_ consumes
+ * (array.cpp:507-622): tile t = ty*n_tiles_x + tx holds tile_rows x
+ * tile_cols pixels row-major, zero-padded where it overhangs the frame —
+ * exactly the bytes Chunk::write_tile_rows (chunk.cpp:17-58) leaves in the
+ * chunk's tile slot, so each tile is ONE contiguous copy into its chunk
+ * buffer.  `tile_nonzero` (optional, n_tiles bytes) receives the chunk zero
+ * scan (1 = some copied byte is nonzero).  `*nbytes` = n_tiles * tile_rows *
+ * tile_cols * bytes_of_type; dst == NULL is a size query (frame stays).
+ */
+int aqz_ds_take_frame_tiled(aqz_ds* ds,
+                            uint32_t level,
+                            uint32_t tile_rows,
+                            uint32_t tile_cols,
+                            void* dst,
+                            size_t cap,
+                            uint8_t* tile_nonzero,
+                            size_t* nbytes,
+                            int* has_frame);
+
+/*
+ * Chunk tiling of a device-resident W x H frame (same layout and scan as
+ * aqz_ds_take_frame_tiled) into device memory `device_tiles`;
+ * `device_nonzero` receives one uint32 per tile.  Runs on `hip_stream`
+ * (NULL = default stream), asynchronous.  For the full-resolution level, whose
+ * tiling the reference does on the host (array.cpp:575 OpenMP loop).
+ */
+int aqz_tile_frame_device(int dtype,
+                          const void* device_frame,
+                          uint32_t width,
+                          uint32_t height,
+                          uint32_t tile_rows,
+                          uint32_t tile_cols,
+                          void* device_tiles,
+                          uint32_t* device_nonzero,
+                          void* hip_stream);
+
+/*
  * Device-resident batch path (benchmark / bulk API).  Equivalent to calling
  * aqz_ds_add_frame on `n_frames` consecutive frames of `device_frames`
  * (frame i at byte offset i*frame_bytes) followed by take_frame on every

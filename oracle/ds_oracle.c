@@ -598,3 +598,50 @@ oracle_ds_level_count(const oracle_ds* ds, uint32_t level)
 {
     return level < ds->n_levels ? ds->count[level] : 0;
 }
+
+/* ---- chunk tiling (array.cpp:507-622, chunk.cpp:17-58) ----------------- */
+
+int
+oracle_tile_frame(int dtype,
+                  const void* src,
+                  uint32_t width,
+                  uint32_t height,
+                  uint32_t tile_rows,
+                  uint32_t tile_cols,
+                  void* dst,
+                  uint8_t* nonzero)
+{
+    const size_t bpp = oracle_bytes_of_type(dtype);
+    if (!bpp || !src || !dst || tile_rows == 0 || tile_cols == 0)
+        return -1;
+    const uint32_t n_tiles_x = (width + tile_cols - 1) / tile_cols;
+    const uint32_t n_tiles_y = (height + tile_rows - 1) / tile_rows;
+    const size_t tile_bytes = (size_t)tile_rows * tile_cols * bpp;
+    const size_t src_row_stride = (size_t)width * bpp;
+    const size_t dst_row_stride = (size_t)tile_cols * bpp; /* bytes_per_tile_row */
+    memset(dst, 0, tile_bytes * n_tiles_x * n_tiles_y);
+    for (uint32_t t = 0; t < n_tiles_x * n_tiles_y; ++t) {
+        const uint32_t ty = t / n_tiles_x, tx = t % n_tiles_x;
+        const uint32_t row0 = ty * tile_rows;
+        uint8_t any = 0;
+        if (row0 < height) {
+            const uint32_t n_rows =
+              tile_rows < height - row0 ? tile_rows : height - row0;
+            const uint32_t col0 = tx * tile_cols;
+            const uint32_t end = col0 + tile_cols < width ? col0 + tile_cols : width;
+            const size_t copy = (size_t)(end - col0) * bpp;
+            const uint8_t* s = (const uint8_t*)src +
+                               ((size_t)row0 * width + col0) * bpp;
+            uint8_t* d = (uint8_t*)dst + t * tile_bytes;
+            for (uint32_t r = 0; r < n_rows; ++r) {
+                const uint8_t* sr = s + r * src_row_stride;
+                memcpy(d + r * dst_row_stride, sr, copy);
+                for (size_t b = 0; !any && b < copy; ++b)
+                    any = sr[b] != 0;
+            }
+        }
+        if (nonzero)
+            nonzero[t] = any;
+    }
+    return 0;
+}

@@ -84,6 +84,24 @@ int oracle_plan_levels(const oracle_dim* dims,
                        uint32_t out_cap_levels,
                        uint32_t* n_levels);
 
+/*
+ * Chunk tiling of one frame (§8(f) row 2 oracle): restates
+ * Array::write_frame_to_chunks_ (array.cpp:507-622) and
+ * Chunk::write_tile_rows (chunk.cpp:17-58) for one row-major frame, written
+ * into a zeroed tile-major buffer — tile t = ty*n_tiles_x + tx at
+ * t*tile_rows*tile_cols*bpp, rows at tile_cols*bpp — exactly the bytes the
+ * reference leaves in each chunk buffer's tile slot.  `nonzero[t]` is the
+ * chunk zero scan (any copied byte != 0).  Returns 0 / -1.
+ */
+int oracle_tile_frame(int dtype,
+                      const void* src,
+                      uint32_t width,
+                      uint32_t height,
+                      uint32_t tile_rows,
+                      uint32_t tile_cols,
+                      void* dst,
+                      uint8_t* nonzero);
+
 /* Stateful downsampler: Downsampler::add_frame / take_frame
  * (downsampler.cpp:306-414) over per-level (width, height, planes). */
 typedef struct oracle_ds oracle_ds;

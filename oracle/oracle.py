@@ -63,6 +63,7 @@ def lib():
         L.oracle_ds_destroy.argtypes = [vp]
         L.oracle_ds_add_frame.argtypes = [vp, vp, sz]
         L.oracle_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz)]
+        L.oracle_tile_frame.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, vp, vp]
         L.oracle_ds_level_count.argtypes = [vp, u32]
         L.oracle_ds_level_count.restype = u32
         _lib = L
@@ -180,6 +181,21 @@ class OracleDownsampler:
 
     def level_count(self, level: int) -> int:
         return lib().oracle_ds_level_count(self._h, level)
+
+
+def tile_frame(img: np.ndarray, tile_rows: int, tile_cols: int):
+    """Chunk tiling of one frame (array.cpp:507-622, chunk.cpp:17-58):
+    returns (tiles[n_tiles, tile_rows, tile_cols], nonzero[n_tiles])."""
+    img = np.ascontiguousarray(img)
+    h, w = img.shape
+    nty, ntx = -(-h // tile_rows), -(-w // tile_cols)
+    out = np.empty((nty * ntx, tile_rows, tile_cols), dtype=img.dtype)
+    nz = np.empty(nty * ntx, dtype=np.uint8)
+    rc = lib().oracle_tile_frame(dtype_code(img.dtype), img.ctypes.data, w, h,
+                                 tile_rows, tile_cols, out.ctypes.data, nz.ctypes.data)
+    if rc:
+        raise ValueError("oracle_tile_frame failed")
+    return out, nz.astype(bool)
 
 
 def cascade_2d(frame: np.ndarray, n_levels: int, method: int):

@@ -405,3 +405,59 @@ def test_full_size_configs_vs_oracle(aqz, oracle, name, method):
                 assert_parity(got[L][k[L]], r, f"{name} m{method} L{L} #{k[L]}")
                 k[L] += 1
     assert [k[L] for L in got] == [counts[L] for L in got]
+
+
+TILE_CASES = [
+    # (level-0 w, h, levels, dtype, tile_rows, tile_cols)
+    (64, 48, 3, np.uint16, 16, 16),      # reference array tests' 16x16 chunks
+    (1000, 600, 4, np.float32, 64, 128),  # ragged tiles at every level
+    (300, 7, 2, np.uint8, 4, 128),
+    (4096, 4096, 5, np.uint16, 256, 256),  # headline chunking
+    (257, 129, 3, np.int64, 32, 32),
+]
+
+
+@pytest.mark.parametrize("case", TILE_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{np.dtype(c[3]).name}")
+def test_take_frame_tiled(aqz, oracle, case):
+    """Chunk-tiled take (§8(f) row 2) equals the oracle's restatement of
+    write_frame_to_chunks_ + write_tile_rows, zero scan included; some tiles
+    are forced all-zero."""
+    w, h, nl, dt, tr, tc = case
+    geo = halving_geometry(w, h, nl)
+    rng = np.random.default_rng(seed_of("tiled", w, h))
+    frame = random_frames(rng, dt, (h, w), specials=False)
+    frame[: h // 2, : w // 2] = 0  # zero tiles at every level
+    ds = aqz.Downsampler(geo, dt, 1)
+    ref = oracle.OracleDownsampler(geo, dt, 1)
+    ds.add_frame(frame)
+    ref.add_frame(frame)
+    for L in range(1, nl):
+        got = ds.take_frame_tiled(L, tr, tc)
+        want_frame = ref.take_frame(L)
+        tiles, nz = oracle.tile_frame(want_frame, tr, tc)
+        assert got is not None
+        assert_parity(got[0], tiles, f"tiles L{L}")
+        assert np.array_equal(got[1], nz), f"zero scan L{L}"
+        assert ds.take_frame(L) is None  # the tiled take consumed the frame
+
+
+def test_tile_frame_device_full_resolution(aqz, oracle):
+    """aqz_tile_frame_device on a full-resolution 4096^2 u16 frame with the
+    headline's 256x256 chunks (the tiling the reference does with OpenMP on the
+    host, array.cpp:575)."""
+    torch = torch_cuda()
+    rng = np.random.default_rng(11)
+    frame = rng.integers(0, 65536, (4096, 4096), dtype=np.uint16)
+    frame[:256, :512] = 0
+    d_in = to_device(frame)
+    nt = 16 * 16
+    d_tiles = empty_device(nt * 256 * 256 * 2)
+    d_nz = torch.zeros(nt, dtype=torch.int32, device="cuda")
+    s = launch_stream()
+    aqz.tile_frame_device(np.uint16, d_in.data_ptr(), 4096, 4096, 256, 256,
+                          d_tiles.data_ptr(), d_nz.data_ptr(), s)
+    torch.cuda.synchronize()
+    tiles, nz = oracle.tile_frame(frame, 256, 256)
+    assert_parity(from_device(d_tiles, np.uint16, (nt, 256, 256)), tiles, "L0 tiles")
+    assert np.array_equal(d_nz.cpu().numpy() != 0, nz)
+    assert not nz[0] and not nz[1] and nz[2:].all()

@@ -158,3 +158,23 @@ def test_emplace_does_not_overwrite(oracle):
     assert ds.level_count(1) == 2
     assert np.all(ds.take_frame(1) == 10)
     assert ds.take_frame(1) is None
+
+
+def test_tile_frame_geometry_and_bytes(oracle):
+    """Chunk tiling oracle: the reference's array tests use 64x48 frames in
+    16x16 chunks -> 4x3 tiles (tests/unit-tests/array-write-even.cpp:26-29);
+    ragged tiles are zero-padded in the chunk buffer; the nonzero flag is the
+    chunk zero scan.  Checked against an independent numpy pad+reshape."""
+    rng = np.random.default_rng(3)
+    for (h, w, tr, tc, dt) in [(48, 64, 16, 16, np.uint16), (50, 70, 16, 32, np.float32),
+                               (7, 300, 4, 128, np.uint8), (33, 33, 64, 64, np.int64)]:
+        img = rng.integers(1, 100, (h, w)).astype(dt)
+        img[:tr, :tc] = 0  # an all-zero first tile
+        tiles, nz = oracle.tile_frame(img, tr, tc)
+        nty, ntx = -(-h // tr), -(-w // tc)
+        assert tiles.shape == (nty * ntx, tr, tc)
+        pad = np.zeros((nty * tr, ntx * tc), dt)
+        pad[:h, :w] = img
+        want = pad.reshape(nty, tr, ntx, tc).transpose(0, 2, 1, 3).reshape(-1, tr, tc)
+        np.testing.assert_array_equal(tiles, want)
+        assert not nz[0] and nz[1:].all()
