@@ -915,46 +915,61 @@ aqz_ds_run_host_batch(aqz_ds* ds,
     const uint8_t* src = static_cast<const uint8_t*>(host_frames);
     int rc = AQZ_OK;
     uint32_t k = 0;
+    // Any failure below still drains all three streams before returning, so
+    // no copy is left reading or writing the caller's buffers.
+    auto drain = [&](int code) {
+        (void)hipStreamSynchronize(p.s_in);
+        (void)hipStreamSynchronize(p.s_work);
+        (void)hipStreamSynchronize(p.s_out);
+        return code;
+    };
+#define HIP_TRY_DRAIN(ds, expr, what)                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess)                                                  \
+            return drain((ds)->fail(e_, what));                                \
+    } while (0)
     for (uint32_t f0 = 0; f0 < n_frames && rc == AQZ_OK; f0 += group, ++k) {
         const int b = int(k & 1);
         const uint32_t g = std::min(group, n_frames - f0);
         // upload: buffer b is free once group k-2's kernels are done with it
-        HIP_TRY(ds, hipStreamWaitEvent(p.s_in, p.work_done[b], 0), "wait");
-        HIP_TRY(ds,
+        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_in, p.work_done[b], 0), "wait");
+        HIP_TRY_DRAIN(ds,
                 hipMemcpyAsync(p.d_in[b], src + size_t(f0) * ds->bytes[0],
                                size_t(g) * ds->bytes[0], hipMemcpyHostToDevice,
                                p.s_in),
                 "hipMemcpyAsync H2D");
-        HIP_TRY(ds, hipEventRecord(p.in_done[b], p.s_in), "event");
+        HIP_TRY_DRAIN(ds, hipEventRecord(p.in_done[b], p.s_in), "event");
         // kernels: after the upload, and after group k-2's download of d_out[b]
-        HIP_TRY(ds, hipStreamWaitEvent(p.s_work, p.in_done[b], 0), "wait");
-        HIP_TRY(ds, hipStreamWaitEvent(p.s_work, p.out_done[b], 0), "wait");
+        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_work, p.in_done[b], 0), "wait");
+        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_work, p.out_done[b], 0), "wait");
         std::vector<uint32_t> counts(ds->n, 0);
         rc = aqz_ds_run_device_batch(ds, p.d_in[b], g, p.d_out[b].data(),
                                      counts.data(), p.s_work);
         if (rc)
-            break;
-        HIP_TRY(ds, hipEventRecord(p.work_done[b], p.s_work), "event");
+            return drain(rc);
+        HIP_TRY_DRAIN(ds, hipEventRecord(p.work_done[b], p.s_work), "event");
         // download every frame this group emitted, appended per level
-        HIP_TRY(ds, hipStreamWaitEvent(p.s_out, p.work_done[b], 0), "wait");
+        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_out, p.work_done[b], 0), "wait");
         for (uint32_t l = 1; l < ds->n; ++l) {
             if (!counts[l])
                 continue;
             uint8_t* dst = static_cast<uint8_t*>(host_out_levels[l]) +
                            size_t(total[l]) * ds->bytes[l];
-            HIP_TRY(ds,
+            HIP_TRY_DRAIN(ds,
                     hipMemcpyAsync(dst, p.d_out[b][l], size_t(counts[l]) * ds->bytes[l],
                                    hipMemcpyDeviceToHost, p.s_out),
                     "hipMemcpyAsync D2H");
             total[l] += counts[l];
         }
-        HIP_TRY(ds, hipEventRecord(p.out_done[b], p.s_out), "event");
+        HIP_TRY_DRAIN(ds, hipEventRecord(p.out_done[b], p.s_out), "event");
     }
-    HIP_TRY(ds, hipStreamSynchronize(p.s_out), "hipStreamSynchronize");
+    drain(AQZ_OK);
     total[0] = n_frames;
     if (out_counts)
         std::copy(total.begin(), total.end(), out_counts);
     return rc;
+#undef HIP_TRY_DRAIN
 }
 
 int
