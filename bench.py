@@ -136,6 +136,10 @@ def parse():
                    help="skip the one-frame oracle spot check")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE traffic passes")
+    p.add_argument("--sink", default="",
+                   help="directory: also time the streaming path with every level "
+                        "frame written to a per-level raw file by a writer thread "
+                        "(BASELINE config C2's filesystem sink)")
     p.add_argument("--xgmi-scatter", action="store_true",
                    help="N>1 only (BASELINE config F): every step, rank 0 scatters "
                         "the ranks' frames over xGMI with RCCL p2p and gathers "
@@ -310,6 +314,10 @@ def main():
                               tile=(chunk, chunk))
             e2e["pipelined"] = measure_e2e_pipelined(aqz, torch, geo, dtype, method,
                                                      d_in, min(B, 64), device)
+            if args.sink:
+                e2e["filesystem_sink"] = measure_e2e_sink(aqz, geo, dtype, method,
+                                                          args.e2e_frames, device,
+                                                          args.sink)
 
     if rank == 0:
         metric = HEADLINE_METRIC if args.workload == "4096x4096_u16" else (
@@ -468,6 +476,52 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
         res["tile"] = list(tile)
     ds.close()
     return res
+
+
+def measure_e2e_sink(aqz, geo, dtype, method, n_frames, device, sink_dir):
+    """Streaming drop-in path into a filesystem sink: add_frame + take_frame
+    of every level, each level frame handed to a writer thread that appends
+    it to <sink_dir>/level_<L>.raw (the reference's sink writes on pool
+    threads, array.cpp:664-811).  Timed to the last byte written and fsync'd.
+    Raw level buffers stand in for Zarr chunks: the full acquire-zarr library
+    (blosc, crc32c, minio-cpp, nlohmann) cannot be built here."""
+    import concurrent.futures as cf
+    import shutil
+    W, H, _ = geo[0]
+    os.makedirs(sink_dir, exist_ok=True)
+    rng = np.random.default_rng(4)
+    if np.dtype(dtype).kind == "f":
+        frames = [rng.uniform(-1000, 1000, (H, W)).astype(dtype) for _ in range(4)]
+    else:
+        frames = [rng.integers(0, np.iinfo(dtype).max, (H, W), dtype=dtype,
+                               endpoint=True) for _ in range(4)]
+    files = {L: open(os.path.join(sink_dir, f"level_{L}.raw"), "wb")
+             for L in range(1, len(geo))}
+    ds = aqz.Downsampler(geo, dtype, method, device=device)
+    written = 0
+    with cf.ThreadPoolExecutor(max_workers=2) as pool:
+        futs = []
+        t0 = time.perf_counter()
+        for i in range(n_frames):
+            ds.add_frame(frames[i % 4])
+            for L in range(1, len(geo)):
+                f = ds.take_frame(L)
+                if f is not None:
+                    futs.append(pool.submit(files[L].write, f.tobytes()))
+                    written += f.nbytes
+        for fu in futs:
+            fu.result()
+        for fh in files.values():
+            fh.flush()
+            os.fsync(fh.fileno())
+        el = time.perf_counter() - t0
+    for fh in files.values():
+        fh.close()
+    ds.close()
+    shutil.rmtree(sink_dir, ignore_errors=True)
+    return {"value": round(n_frames * W * H / el / 1e9, 3), "unit": "GPixels/s",
+            "ms_per_frame": round(el / n_frames * 1e3, 3), "bytes_written": written,
+            "path": "add_frame + take_frame + writer thread -> per-level raw files, fsync"}
 
 
 def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device):
