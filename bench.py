@@ -122,8 +122,8 @@ def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="4096x4096_u16", choices=sorted(WORKLOADS))
     p.add_argument("--batch", type=int, default=0,
                    help="frames (planes) per step per GPU; 0 = workload default")
