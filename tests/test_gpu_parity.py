@@ -461,3 +461,63 @@ def test_tile_frame_device_full_resolution(aqz, oracle):
     assert_parity(from_device(d_tiles, np.uint16, (nt, 256, 256)), tiles, "L0 tiles")
     assert np.array_equal(d_nz.cpu().numpy() != 0, nz)
     assert not nz[0] and not nz[1] and nz[2:].all()
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32, np.float64],
+                         ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("method", METHODS)
+def test_degenerate_frames(aqz, oracle, dtype, method):
+    """Edge geometries: 1-pixel-wide and 1-pixel-tall frames (the right or
+    bottom neighbour is always the replicated edge), 1x1 levels, 2x2 -> 1x1."""
+    rng = np.random.default_rng(seed_of("degenerate", np.dtype(dtype).name, method))
+    for geo in ([(1, 100, 1), (1, 50, 1), (1, 25, 1)],
+                [(100, 1, 1), (50, 1, 1), (25, 1, 1)],
+                [(2, 2, 1), (1, 1, 1)],
+                [(3, 3, 1), (2, 2, 1), (1, 1, 1)],
+                [(1, 1, 4), (1, 1, 2)]):
+        w, h, z = geo[0]
+        frames = [random_frames(rng, dtype, (h, w)) for _ in range(max(2, z))]
+        got, want = run_both(aqz, oracle, geo, dtype, method, frames)
+        assert len(got) == len(want)
+        for (i, L, a), (_, _, b) in zip(got, want):
+            assert_parity(a, b, f"{geo} f{i} L{L}")
+
+
+def test_single_level_and_errors(aqz):
+    """A one-level handle (no pyramid) emits nothing; wrong frame sizes and
+    levels are rejected the way the reference's EXPECTs reject them."""
+    ds = aqz.Downsampler([(64, 64, 1)], np.uint16, 1)
+    ds.add_frame(np.zeros((64, 64), np.uint16))
+    assert ds.take_frame(1) is None and ds.take_frame(0) is None
+    ds = aqz.Downsampler(halving_geometry(64, 64, 3), np.uint16, 1)
+    with pytest.raises(aqz.AqzError) as e:
+        ds.add_frame(np.zeros((64, 63), np.uint16))
+    assert e.value.status == 1
+    with pytest.raises(TypeError):
+        ds.add_frame(np.zeros((64, 64), np.uint8))
+    assert ds.take_frame(7) is None and ds.take_frame(-1) is None
+    ds.add_frame(np.ones((64, 64), np.uint16))
+    assert np.all(ds.take_frame(2) == 1)
+
+
+def test_max_size_frame_two_fused_runs(aqz, oracle):
+    """16384^2 u16 with 64-px chunks: the planner gives 9 levels, i.e. one
+    4-level cascade launch chained into a second 4-level launch from level 4
+    (512 MiB frame), bit-exact against the oracle."""
+    torch = torch_cuda()
+    dims = [(aqz.TIME, 0, 1, 1), (aqz.SPACE, 16384, 64, 1), (aqz.SPACE, 16384, 64, 1)]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    assert len(geo) == 9 and geo[-1][:2] == (64, 64)
+    rng = np.random.default_rng(16384)
+    frame = rng.integers(0, 65536, (16384, 16384), dtype=np.uint16)
+    d_in = to_device(frame)
+    outs = [None] + [empty_device(w * h * 2) for w, h, _ in geo[1:]]
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ds.run_device_batch(d_in.data_ptr(), 1, [0] + [o.data_ptr() for o in outs[1:]],
+                        launch_stream())
+    torch.cuda.synchronize()
+    assert ds.last_batch_kind() == 1
+    ref = oracle.cascade_2d(frame, 9, 1)
+    for L in range(1, 9):
+        w, h, _ = geo[L]
+        assert_parity(from_device(outs[L], np.uint16, (h, w)), ref[L - 1], f"L{L}")
