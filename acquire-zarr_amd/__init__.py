@@ -34,7 +34,7 @@ EXPORTS = (
     "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
     "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
-    "aqz_tile_frame_device",
+    "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -89,6 +89,7 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(u32), vp]
     L.aqz_ds_take_frame_tiled.argtypes = [vp, u32, u32, u32, vp, sz, vp,
                                           ctypes.POINTER(sz), ctypes.POINTER(i32)]
+    L.aqz_ds_set_level_tiling.argtypes = [vp, u32, u32, u32]
     L.aqz_tile_frame_device.argtypes = [i32, vp, u32, u32, u32, u32, vp, vp, vp]
     L.aqz_ds_run_host_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
                                         ctypes.POINTER(u32)]
@@ -204,6 +205,9 @@ class Downsampler:
 
     def level_bytes(self, level: int) -> int:
         return lib().aqz_ds_level_bytes(self._h, level)
+
+    def set_level_tiling(self, level: int, tile_rows: int, tile_cols: int):
+        self._check(lib().aqz_ds_set_level_tiling(self._h, level, tile_rows, tile_cols))
 
     def take_frame_tiled(self, level: int, tile_rows: int, tile_cols: int):
         """Chunk-tiled take: (tiles[n_tiles, tile_rows, tile_cols],

@@ -115,6 +115,20 @@ hipError_t launch_tile_frame(int dtype,
                              uint32_t* nonzero,
                              hipStream_t stream);
 
+// Same tiling with one flag byte per (tile, slice): slice_flags holds
+// n_tiles * tile_slices(tile_rows, tile_cols) bytes (tile-major), written
+// without atomics or a pre-clear; a tile is nonzero iff any of its slices is.
+uint32_t tile_slices(uint32_t tile_rows, uint32_t tile_cols);
+hipError_t launch_tile_frame_sliced(int dtype,
+                                    const void* src,
+                                    uint32_t W,
+                                    uint32_t H,
+                                    uint32_t tile_rows,
+                                    uint32_t tile_cols,
+                                    void* dst,
+                                    uint8_t* slice_flags,
+                                    hipStream_t stream);
+
 // Tuning knob for the cascade grid (waves resident per CU × CUs); 0 = auto.
 void set_cascade_grid_cap(uint32_t blocks);
 

@@ -633,7 +633,10 @@ nonzero_bits(T v)
     }
 }
 
-template<typename T>
+// SLICE_FLAGS: every block writes its own flag byte (flags[t*slices + s]),
+// no atomics and no pre-clear; otherwise one u32 per tile, OR-ed atomically
+// (the caller clears it).
+template<typename T, bool SLICE_FLAGS>
 __global__ __launch_bounds__(256) void
 tile_kernel(const T* __restrict__ src,
             uint32_t W,
@@ -643,7 +646,7 @@ tile_kernel(const T* __restrict__ src,
             uint32_t n_tiles_x,
             uint32_t slices,
             T* __restrict__ dst,
-            uint32_t* __restrict__ nonzero)
+            void* __restrict__ flags)
 {
     const uint32_t t = blockIdx.x / slices;
     const uint32_t s = blockIdx.x % slices;
@@ -666,8 +669,14 @@ tile_kernel(const T* __restrict__ src,
         }
         out[e] = v;
     }
-    if (__syncthreads_or(any) && threadIdx.x == 0)
-        atomicOr(nonzero + t, 1u);
+    const bool block_any = __syncthreads_or(any);
+    if (threadIdx.x == 0) {
+        if constexpr (SLICE_FLAGS) {
+            static_cast<uint8_t*>(flags)[blockIdx.x] = block_any ? 1 : 0;
+        } else if (block_any) {
+            atomicOr(static_cast<uint32_t*>(flags) + t, 1u);
+        }
+    }
 }
 
 // ---- dispatch ---------------------------------------------------------------
@@ -939,6 +948,57 @@ launch_volume(int dtype,
     });
 }
 
+uint32_t
+tile_slices(uint32_t tile_rows, uint32_t tile_cols)
+{
+    // ~8 K elements per block, at most 64 blocks per tile
+    const uint64_t tile_elems = uint64_t(tile_rows) * tile_cols;
+    return uint32_t(std::min<uint64_t>(64, std::max<uint64_t>(1, tile_elems / 8192)));
+}
+
+namespace {
+
+hipError_t
+launch_tile_impl(int dtype,
+                 const void* src,
+                 uint32_t W,
+                 uint32_t H,
+                 uint32_t tile_rows,
+                 uint32_t tile_cols,
+                 void* dst,
+                 void* flags,
+                 bool slice_flags,
+                 hipStream_t stream)
+{
+    if (W == 0 || H == 0 || tile_rows == 0 || tile_cols == 0)
+        return hipErrorInvalidValue;
+    const uint32_t ntx = (W + tile_cols - 1) / tile_cols;
+    const uint32_t nty = (H + tile_rows - 1) / tile_rows;
+    const uint32_t slices = tile_slices(tile_rows, tile_cols);
+    const uint64_t blocks = uint64_t(ntx) * nty * slices;
+    if (blocks >= (1ull << 31))
+        return hipErrorInvalidValue;
+    if (!slice_flags) {
+        hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * ntx * nty, stream);
+        if (e != hipSuccess)
+            return e;
+    }
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        if (slice_flags)
+            hipLaunchKernelGGL((tile_kernel<T, true>), dim3(uint32_t(blocks)), dim3(256),
+                               0, stream, static_cast<const T*>(src), W, H, tile_rows,
+                               tile_cols, ntx, slices, static_cast<T*>(dst), flags);
+        else
+            hipLaunchKernelGGL((tile_kernel<T, false>), dim3(uint32_t(blocks)), dim3(256),
+                               0, stream, static_cast<const T*>(src), W, H, tile_rows,
+                               tile_cols, ntx, slices, static_cast<T*>(dst), flags);
+        return hipGetLastError();
+    });
+}
+
+} // namespace
+
 hipError_t
 launch_tile_frame(int dtype,
                   const void* src,
@@ -950,27 +1010,23 @@ launch_tile_frame(int dtype,
                   uint32_t* nonzero,
                   hipStream_t stream)
 {
-    if (W == 0 || H == 0 || tile_rows == 0 || tile_cols == 0)
-        return hipErrorInvalidValue;
-    const uint32_t ntx = (W + tile_cols - 1) / tile_cols;
-    const uint32_t nty = (H + tile_rows - 1) / tile_rows;
-    const uint64_t tile_elems = uint64_t(tile_rows) * tile_cols;
-    // ~8 K elements per block, at most 64 blocks per tile
-    const uint32_t slices =
-      uint32_t(std::min<uint64_t>(64, std::max<uint64_t>(1, tile_elems / 8192)));
-    const uint64_t blocks = uint64_t(ntx) * nty * slices;
-    if (blocks >= (1ull << 31))
-        return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(nonzero, 0, sizeof(uint32_t) * ntx * nty, stream);
-    if (e != hipSuccess)
-        return e;
-    return with_dtype(dtype, [&](auto tag) -> hipError_t {
-        using T = decltype(tag);
-        hipLaunchKernelGGL((tile_kernel<T>), dim3(uint32_t(blocks)), dim3(256), 0,
-                           stream, static_cast<const T*>(src), W, H, tile_rows,
-                           tile_cols, ntx, slices, static_cast<T*>(dst), nonzero);
-        return hipGetLastError();
-    });
+    return launch_tile_impl(dtype, src, W, H, tile_rows, tile_cols, dst, nonzero,
+                            false, stream);
+}
+
+hipError_t
+launch_tile_frame_sliced(int dtype,
+                         const void* src,
+                         uint32_t W,
+                         uint32_t H,
+                         uint32_t tile_rows,
+                         uint32_t tile_cols,
+                         void* dst,
+                         uint8_t* slice_flags,
+                         hipStream_t stream)
+{
+    return launch_tile_impl(dtype, src, W, H, tile_rows, tile_cols, dst, slice_flags,
+                            true, stream);
 }
 
 hipError_t

@@ -109,11 +109,18 @@ struct aqz_ds
     size_t device_bytes = 0;
     int last_batch_kind = -1;
 
-    // aqz_ds_take_frame_tiled scratch, grown on demand
+    // aqz_ds_take_frame_tiled: on-demand scratch (tiles, then slice flags)
     void* d_tiles = nullptr;
     size_t d_tiles_bytes = 0;
-    uint32_t* d_nonzero = nullptr;
-    size_t d_nonzero_n = 0;
+    // aqz_ds_set_level_tiling: per level (tile_rows, tile_cols), two tiled
+    // slots (tiles then slice flags) paired with `slot`, and which slot's
+    // frame they currently hold (-1 none)
+    std::vector<std::pair<uint32_t, uint32_t>> tiling;
+    std::vector<std::pair<void*, void*>> tslot;
+    std::vector<std::pair<uint8_t*, uint8_t*>> tflags; // pinned, kernel-written
+    std::vector<int> tiled_for;
+    uint8_t* h_flags = nullptr; // pinned slice flags for on-demand tiling
+    size_t h_flags_bytes = 0;
 
     // aqz_ds_run_host_batch pipeline, allocated on first use
     struct Pipe
@@ -170,6 +177,21 @@ elems(const aqz_ds* ds, uint32_t level)
     return uint64_t(ds->lv[level].width) * ds->lv[level].height;
 }
 
+// Tiled layout of level L at (tr, tc): tile bytes and slice-flag bytes.
+struct TileGeom
+{
+    size_t n_tiles, tile_bytes, flag_bytes;
+};
+
+TileGeom
+tile_geom(const aqz_ds* ds, uint32_t L, uint32_t tr, uint32_t tc)
+{
+    const aqz_level_desc& lv = ds->lv[L];
+    const size_t ntx = (lv.width + tc - 1) / tc, nty = (lv.height + tr - 1) / tr;
+    const size_t nt = ntx * nty;
+    return { nt, nt * tr * tc * ds->bpp, nt * aqz::tile_slices(tr, tc) };
+}
+
 // Working buffer for a level-L result: the caller's batch slot when the
 // sink is a batch, else the level's free device slot.
 void*
@@ -199,8 +221,22 @@ emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink)
     }
     // unordered_map::emplace keeps an untaken frame; the new one is dropped
     // (it stays in the free slot only as the next level's input).
-    if (ds->cached[level] < 0)
-        ds->cached[level] = (want == ds->slot[level].first) ? 0 : 1;
+    if (ds->cached[level] < 0) {
+        const int k = (want == ds->slot[level].first) ? 0 : 1;
+        ds->cached[level] = k;
+        const auto [tr, tc] = ds->tiling[level];
+        if (tr) {
+            // queue the chunk tiling right behind the pyramid (§8(f) row 2)
+            void* tb = k == 0 ? ds->tslot[level].first : ds->tslot[level].second;
+            uint8_t* fb = k == 0 ? ds->tflags[level].first : ds->tflags[level].second;
+            HIP_TRY(ds,
+                    aqz::launch_tile_frame_sliced(ds->dtype, want, ds->lv[level].width,
+                                                  ds->lv[level].height, tr, tc, tb, fb,
+                                                  ds->stream),
+                    "tile kernel");
+            ds->tiled_for[level] = k;
+        }
+    }
     return AQZ_OK;
 }
 
@@ -345,7 +381,15 @@ release(aqz_ds* ds)
         (void)hipFree(p);
     (void)hipHostFree(ds->h_stage);
     (void)hipFree(ds->d_tiles);
-    (void)hipFree(ds->d_nonzero);
+    for (auto& t : ds->tslot) {
+        (void)hipFree(t.first);
+        (void)hipFree(t.second);
+    }
+    for (auto& t : ds->tflags) {
+        (void)hipHostFree(t.first);
+        (void)hipHostFree(t.second);
+    }
+    (void)hipHostFree(ds->h_flags);
     if (ds->h2d_done)
         (void)hipEventDestroy(ds->h2d_done);
     for (int b = 0; b < 2; ++b) {
@@ -493,6 +537,10 @@ aqz_ds_create(const aqz_level_desc* levels,
     ds->cached.assign(n_levels, -1);
     ds->d_partial.assign(n_levels, nullptr);
     ds->staged = env_flag("AQZ_PINNED_STAGING");
+    ds->tiling.assign(n_levels, { 0, 0 });
+    ds->tslot.assign(n_levels, { nullptr, nullptr });
+    ds->tflags.assign(n_levels, { nullptr, nullptr });
+    ds->tiled_for.assign(n_levels, -1);
     for (uint32_t l = 0; l < n_levels; ++l) {
         ds->bytes[l] = size_t(levels[l].width) * levels[l].height * ds->bpp;
         if (l > 0) {
@@ -622,6 +670,44 @@ aqz_ds_take_frame(aqz_ds* ds,
             "hipMemcpyAsync D2H");
     HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
     ds->cached[level] = -1;
+    ds->tiled_for[level] = -1;
+    return AQZ_OK;
+}
+
+int
+aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t tile_cols)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (level == 0 || level >= ds->n)
+        return ds->fail_arg("set_level_tiling: bad level " + std::to_string(level));
+    if ((tile_rows == 0) != (tile_cols == 0))
+        return ds->fail_arg("set_level_tiling: tile rows/cols must both be 0 or >0");
+    if (int rc = bind_device(ds))
+        return rc;
+    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+    auto& t = ds->tslot[level];
+    (void)hipFree(t.first);
+    (void)hipFree(t.second);
+    t = { nullptr, nullptr };
+    auto& tf = ds->tflags[level];
+    (void)hipHostFree(tf.first);
+    (void)hipHostFree(tf.second);
+    tf = { nullptr, nullptr };
+    ds->tiling[level] = { 0, 0 };
+    ds->tiled_for[level] = -1;
+    if (tile_rows == 0)
+        return AQZ_OK;
+    const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
+    HIP_TRY(ds, hipMalloc(&t.first, g.tile_bytes), "hipMalloc tiles");
+    HIP_TRY(ds, hipMalloc(&t.second, g.tile_bytes), "hipMalloc tiles");
+    // slice flags live in pinned host memory the kernel writes directly, so
+    // take_frame_tiled needs no separate flag copy
+    HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.first), g.flag_bytes,
+                              hipHostMallocDefault), "hipHostMalloc flags");
+    HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.second), g.flag_bytes,
+                              hipHostMallocDefault), "hipHostMalloc flags");
+    ds->tiling[level] = { tile_rows, tile_cols };
     return AQZ_OK;
 }
 
@@ -643,52 +729,65 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
         return ds->fail_arg("take_frame_tiled: empty tile");
     if (level == 0 || level >= ds->n || ds->cached[level] < 0)
         return AQZ_OK;
-    const aqz_level_desc& lv = ds->lv[level];
-    const size_t ntx = (lv.width + tile_cols - 1) / tile_cols;
-    const size_t nty = (lv.height + tile_rows - 1) / tile_rows;
-    const size_t bytes = ntx * nty * tile_rows * tile_cols * ds->bpp;
+    const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
     *has_frame = 1;
     if (nbytes)
-        *nbytes = bytes;
+        *nbytes = g.tile_bytes;
     if (!dst)
         return AQZ_OK;
-    if (cap < bytes)
+    if (cap < g.tile_bytes)
         return ds->fail_arg("take_frame_tiled: buffer too small");
     if (int rc = bind_device(ds))
         return rc;
-    if (ds->d_tiles_bytes < bytes) {
-        (void)hipFree(ds->d_tiles);
-        ds->d_tiles = nullptr;
-        ds->d_tiles_bytes = 0;
-        HIP_TRY(ds, hipMalloc(&ds->d_tiles, bytes), "hipMalloc tiles");
-        ds->d_tiles_bytes = bytes;
+    const int k = ds->cached[level];
+    const void* tiles = nullptr;
+    const uint8_t* flags = nullptr;
+    if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
+        ds->tiled_for[level] == k) {
+        // tiled when the frame was emitted (aqz_ds_set_level_tiling)
+        tiles = k == 0 ? ds->tslot[level].first : ds->tslot[level].second;
+        flags = k == 0 ? ds->tflags[level].first : ds->tflags[level].second;
+    } else {
+        // on demand, into the scratch buffers
+        if (ds->d_tiles_bytes < g.tile_bytes) {
+            (void)hipFree(ds->d_tiles);
+            ds->d_tiles = nullptr;
+            ds->d_tiles_bytes = 0;
+            HIP_TRY(ds, hipMalloc(&ds->d_tiles, g.tile_bytes), "hipMalloc tiles");
+            ds->d_tiles_bytes = g.tile_bytes;
+        }
+        if (ds->h_flags_bytes < g.flag_bytes) {
+            (void)hipHostFree(ds->h_flags);
+            ds->h_flags = nullptr;
+            ds->h_flags_bytes = 0;
+            HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&ds->h_flags), g.flag_bytes,
+                                      hipHostMallocDefault), "hipHostMalloc flags");
+            ds->h_flags_bytes = g.flag_bytes;
+        }
+        HIP_TRY(ds,
+                aqz::launch_tile_frame_sliced(ds->dtype, ds->slot_ptr(level, k),
+                                              ds->lv[level].width, ds->lv[level].height,
+                                              tile_rows, tile_cols, ds->d_tiles,
+                                              ds->h_flags, ds->stream),
+                "tile kernel");
+        tiles = ds->d_tiles;
+        flags = ds->h_flags;
     }
-    if (ds->d_nonzero_n < ntx * nty) {
-        (void)hipFree(ds->d_nonzero);
-        ds->d_nonzero = nullptr;
-        ds->d_nonzero_n = 0;
-        HIP_TRY(ds, hipMalloc(&ds->d_nonzero, sizeof(uint32_t) * ntx * nty),
-                "hipMalloc tile flags");
-        ds->d_nonzero_n = ntx * nty;
-    }
     HIP_TRY(ds,
-            aqz::launch_tile_frame(ds->dtype, ds->slot_ptr(level, ds->cached[level]),
-                                   lv.width, lv.height, tile_rows, tile_cols,
-                                   ds->d_tiles, ds->d_nonzero, ds->stream),
-            "tile kernel");
-    HIP_TRY(ds,
-            hipMemcpyAsync(dst, ds->d_tiles, bytes, hipMemcpyDeviceToHost, ds->stream),
-            "hipMemcpyAsync D2H");
-    std::vector<uint32_t> flags(ntx * nty);
-    HIP_TRY(ds,
-            hipMemcpyAsync(flags.data(), ds->d_nonzero, sizeof(uint32_t) * flags.size(),
-                           hipMemcpyDeviceToHost, ds->stream),
+            hipMemcpyAsync(dst, tiles, g.tile_bytes, hipMemcpyDeviceToHost, ds->stream),
             "hipMemcpyAsync D2H");
     HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-    if (tile_nonzero)
-        for (size_t t = 0; t < flags.size(); ++t)
-            tile_nonzero[t] = flags[t] ? 1 : 0;
+    if (tile_nonzero) {
+        const size_t slices = g.flag_bytes / g.n_tiles;
+        for (size_t t = 0; t < g.n_tiles; ++t) {
+            uint8_t any = 0;
+            for (size_t q = 0; q < slices; ++q)
+                any |= flags[t * slices + q];
+            tile_nonzero[t] = any ? 1 : 0;
+        }
+    }
     ds->cached[level] = -1;
+    ds->tiled_for[level] = -1;
     return AQZ_OK;
 }
 

@@ -465,7 +465,10 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
            "frames": n_frames}
     if tile:
         # same loop with the chunk-tiled take: levels
-        # arrive tile-major with the zero scan done on the GPU
+        # are tiled on the GPU behind the pyramid and arrive tile-major with
+        # the zero scan done
+        for L in range(1, len(geo)):
+            ds.set_level_tiling(L, tile[0], tile[1])
         t0 = time.perf_counter()
         for i in range(n_frames):
             ds.add_frame(frames[i % 4])

@@ -198,6 +198,18 @@ int aqz_ds_take_frame_tiled(aqz_ds* ds,
                             int* has_frame);
 
 /*
+ * Declare level `level`'s chunk tile (its chunk_size_px in y and x — chunks
+ * are preserved across levels, downsampler.cpp:16-17).  From then on every
+ * frame that becomes the level's cached frame is also tiled on the GPU right
+ * behind the pyramid kernels, so aqz_ds_take_frame_tiled with the same tile
+ * is a plain device->host copy.  0, 0 switches it off.
+ */
+int aqz_ds_set_level_tiling(aqz_ds* ds,
+                            uint32_t level,
+                            uint32_t tile_rows,
+                            uint32_t tile_cols);
+
+/*
  * Chunk tiling of a device-resident W x H frame (same layout and scan as
  * aqz_ds_take_frame_tiled) into device memory `device_tiles`;
  * `device_nonzero` receives one uint32 per tile.  Runs on `hip_stream`

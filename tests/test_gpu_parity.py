@@ -417,8 +417,9 @@ TILE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("eager", [False, True], ids=["on_demand", "eager"])
 @pytest.mark.parametrize("case", TILE_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{np.dtype(c[3]).name}")
-def test_take_frame_tiled(aqz, oracle, case):
+def test_take_frame_tiled(aqz, oracle, case, eager):
     """Chunk-tiled take (§8(f) row 2) equals the oracle's restatement of
     write_frame_to_chunks_ + write_tile_rows, zero scan included; some tiles
     are forced all-zero."""
@@ -428,6 +429,9 @@ def test_take_frame_tiled(aqz, oracle, case):
     frame = random_frames(rng, dt, (h, w), specials=False)
     frame[: h // 2, : w // 2] = 0  # zero tiles at every level
     ds = aqz.Downsampler(geo, dt, 1)
+    if eager:  # tiles computed behind the pyramid (aqz_ds_set_level_tiling)
+        for L in range(1, nl):
+            ds.set_level_tiling(L, tr, tc)
     ref = oracle.OracleDownsampler(geo, dt, 1)
     ds.add_frame(frame)
     ref.add_frame(frame)
@@ -521,3 +525,28 @@ def test_max_size_frame_two_fused_runs(aqz, oracle):
     for L in range(1, 9):
         w, h, _ = geo[L]
         assert_parity(from_device(outs[L], np.uint16, (h, w)), ref[L - 1], f"L{L}")
+
+
+def test_eager_tiling_follows_the_cached_frame(aqz, oracle):
+    """With eager tiling on, the tiles always belong to the cached frame: an
+    untaken frame keeps its tiles while newer frames are dropped, a plain
+    take_frame consumes the frame, and a different tile shape falls back to
+    on-demand tiling."""
+    geo = halving_geometry(128, 96, 3)
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ds.set_level_tiling(1, 16, 32)
+    ds.set_level_tiling(2, 16, 16)
+    rng = np.random.default_rng(8)
+    f0, f1, f2 = (rng.integers(0, 65536, (96, 128), dtype=np.uint16) for _ in range(3))
+    ds.add_frame(f0)
+    ds.add_frame(f1)  # dropped at both levels: f0 still cached
+    want1 = oracle.cascade_2d(f0, 3, 1)
+    got = ds.take_frame_tiled(1, 16, 32)
+    assert_parity(got[0], oracle.tile_frame(want1[0], 16, 32)[0], "L1 keeps f0")
+    ds.add_frame(f2)  # level 1 now caches f2; level 2 still holds f0
+    want2 = oracle.cascade_2d(f2, 3, 1)
+    got = ds.take_frame_tiled(1, 8, 8)  # other shape: on-demand path
+    assert_parity(got[0], oracle.tile_frame(want2[0], 8, 8)[0], "L1 f2 on demand")
+    assert np.array_equal(ds.take_frame(2), want1[1])  # plain take of f0
+    assert ds.take_frame_tiled(2, 16, 16) is None
+    ds.set_level_tiling(1, 0, 0)
