@@ -35,6 +35,8 @@ EXPORTS = (
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
     "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
+    "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_set_input_transpose",
+    "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -82,6 +84,12 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_destroy.argtypes = [vp]
     L.aqz_ds_destroy.restype = None
     L.aqz_ds_add_frame.argtypes = [vp, vp, sz]
+    L.aqz_ds_add_frame_async.argtypes = [vp, vp, sz]
+    L.aqz_ds_wait.argtypes = [vp]
+    L.aqz_ds_set_input_transpose.argtypes = [vp, ctypes.c_int]
+    L.aqz_ds_take_input_frame.argtypes = [vp, u32, u32, vp, sz, vp, ctypes.POINTER(sz),
+                                          ctypes.POINTER(ctypes.c_int)]
+    L.aqz_transpose_frame_device.argtypes = [ctypes.c_int, vp, u32, u32, vp, vp]
     L.aqz_ds_add_device_frame.argtypes = [vp, vp, sz]
     L.aqz_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz),
                                     ctypes.POINTER(i32)]
@@ -186,6 +194,7 @@ class Downsampler:
             raise AqzError(rc, L.aqz_last_error().decode())
         self._h = h
         self.method = method
+        self._pending = None  # frame of a pending add_frame_async
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -224,6 +233,30 @@ class Downsampler:
             nz.ctypes.data, ctypes.byref(nb), ctypes.byref(has)))
         return (out, nz.astype(bool)) if has.value else None
 
+    def set_input_transpose(self, transpose: bool):
+        """aqz_ds_set_input_transpose: frames arrive in acquisition order
+        (levels[0].width rows x levels[0].height columns)."""
+        self._check(lib().aqz_ds_set_input_transpose(self._h, 1 if transpose else 0))
+
+    def take_input_frame(self, tile_rows: int = 0, tile_cols: int = 0):
+        """Last added level-0 frame in storage order: (h, w) array when
+        untiled, else (tiles, nonzero) like take_frame_tiled; None if none."""
+        w, h, _ = self.geometry[0]
+        nb, has = ctypes.c_size_t(0), ctypes.c_int(0)
+        if tile_rows == 0 and tile_cols == 0:
+            out = np.empty((h, w), dtype=self.dtype)
+            self._check(lib().aqz_ds_take_input_frame(
+                self._h, 0, 0, out.ctypes.data, out.nbytes, None, ctypes.byref(nb),
+                ctypes.byref(has)))
+            return out if has.value else None
+        nt = (-(-h // tile_rows)) * (-(-w // tile_cols))
+        out = np.empty((nt, tile_rows, tile_cols), dtype=self.dtype)
+        nz = np.empty(nt, dtype=np.uint8)
+        self._check(lib().aqz_ds_take_input_frame(
+            self._h, tile_rows, tile_cols, out.ctypes.data, out.nbytes, nz.ctypes.data,
+            ctypes.byref(nb), ctypes.byref(has)))
+        return (out, nz.astype(bool)) if has.value else None
+
     def run_host_batch(self, host_frames: int, n_frames: int, host_outs):
         """Pipelined host batch: `host_frames` and `host_outs[L]` are host
         addresses (index 0 ignored).  Returns frames emitted per level."""
@@ -246,6 +279,22 @@ class Downsampler:
         if frame.dtype != self.dtype:
             raise TypeError(f"frame dtype {frame.dtype} != {self.dtype}")
         self._check(lib().aqz_ds_add_frame(self._h, frame.ctypes.data, frame.nbytes))
+
+    def add_frame_async(self, frame: np.ndarray):
+        """aqz_ds_add_frame_async: returns at once; `frame` is kept alive
+        (and must not be modified) until wait() or the next call."""
+        frame = np.ascontiguousarray(frame)
+        if frame.dtype != self.dtype:
+            raise TypeError(f"frame dtype {frame.dtype} != {self.dtype}")
+        self._pending = frame
+        self._check(lib().aqz_ds_add_frame_async(self._h, frame.ctypes.data,
+                                                 frame.nbytes))
+
+    def wait(self):
+        try:
+            self._check(lib().aqz_ds_wait(self._h))
+        finally:
+            self._pending = None
 
     def add_device_frame(self, device_ptr: int, nbytes: int):
         self._check(lib().aqz_ds_add_device_frame(self._h, device_ptr, nbytes))
@@ -282,6 +331,17 @@ def tile_frame_device(dtype, device_frame: int, width: int, height: int,
     rc = L.aqz_tile_frame_device(dtype_code(dtype), device_frame, width, height,
                                  tile_rows, tile_cols, device_tiles, device_nonzero,
                                  ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+
+
+def transpose_frame_device(dtype, device_src: int, rows: int, cols: int,
+                           device_dst: int, stream: int = 0):
+    """aqz_transpose_frame_device (asynchronous on `stream`)."""
+    L = lib()
+    rc = L.aqz_transpose_frame_device(dtype_code(dtype), device_src, rows, cols,
+                                      device_dst,
+                                      ctypes.c_void_p(stream) if stream else None)
     if rc:
         raise AqzError(rc, L.aqz_last_error().decode())
 

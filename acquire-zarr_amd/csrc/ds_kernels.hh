@@ -102,6 +102,15 @@ hipError_t launch_zpair(int dtype,
                         hipStream_t stream);
 
 // Chunk tiling of one W x H frame (array.cpp:507-622 / chunk.cpp:17-58):
+// transpose_frame (array.cpp:488-504): `dst` (cols x rows, row-major)
+// receives the transpose of `src` (rows x cols, row-major).
+hipError_t launch_transpose(int dtype,
+                            const void* src,
+                            uint32_t rows,
+                            uint32_t cols,
+                            void* dst,
+                            hipStream_t stream);
+
 // `dst` receives n_tiles x tile_rows x tile_cols elements, tile-major,
 // zero-padded; `nonzero[t]` (device, one u32 per tile, cleared here) is set
 // when tile t holds any nonzero byte.

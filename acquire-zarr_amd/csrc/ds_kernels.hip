@@ -679,6 +679,76 @@ tile_kernel(const T* __restrict__ src,
     }
 }
 
+// ---- transpose_frame (array.cpp:488-504) ------------------------------------
+//
+// Y x X -> X x Y of a row-major `rows` x `cols` frame, for arrays whose
+// storage order swaps the two spatial dimensions (Array::write_frame_to_chunks_
+// transposes level 0 before chunking, array.cpp:517-530, and the downsampler
+// then sees the transposed frame).  Pure data movement, HBM-bound:
+// 2 * rows * cols * sizeof(T) bytes.  One block per 64 x 64-element tile,
+// staged through LDS so both the global reads (source rows) and the global
+// writes (destination rows) are contiguous; with VEC each lane moves 16 B per
+// access on interior tiles.  Edge tiles (and VEC=false frames, whose rows are
+// not 16-B aligned) move one element per access.
+
+constexpr int kTransposeTile = 64;
+
+template<typename T>
+constexpr int kTransposePitch = kTransposeTile + (sizeof(T) >= 4 ? 1 : 4 / int(sizeof(T)));
+
+template<typename T, bool VEC>
+__global__ __launch_bounds__(256) void
+transpose_kernel(const T* __restrict__ src, uint32_t rows, uint32_t cols, T* __restrict__ dst)
+{
+    constexpr int TD = kTransposeTile;
+    constexpr int P = kTransposePitch<T>;
+    __shared__ T tile[TD * P];
+    const uint32_t c0 = blockIdx.x * TD; // source columns = destination rows
+    const uint32_t r0 = blockIdx.y * TD; // source rows = destination columns
+    const int tid = threadIdx.x;
+    const bool interior = VEC && r0 + TD <= rows && c0 + TD <= cols;
+    if (interior) {
+        constexpr int V = 16 / int(sizeof(T));
+        constexpr int VPR = TD / V;       // vectors per tile row
+        constexpr int RPP = 256 / VPR;    // tile rows per pass
+        const int v = tid % VPR;
+#pragma unroll
+        for (int r = tid / VPR; r < TD; r += RPP) {
+            const auto* p = reinterpret_cast<const u32x4*>(src + uint64_t(r0 + r) * cols + c0) + v;
+            const u32x4 x = __builtin_nontemporal_load(p);
+            T e[V];
+            __builtin_memcpy(e, &x, 16);
+#pragma unroll
+            for (int k = 0; k < V; ++k)
+                tile[r * P + v * V + k] = e[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = tid / VPR; c < TD; c += RPP) {
+            T e[V];
+#pragma unroll
+            for (int k = 0; k < V; ++k)
+                e[k] = tile[(v * V + k) * P + c];
+            u32x4 x;
+            __builtin_memcpy(&x, e, 16);
+            auto* q = reinterpret_cast<u32x4*>(dst + uint64_t(c0 + c) * rows + r0) + v;
+            __builtin_nontemporal_store(x, q);
+        }
+    } else {
+        // one element per access; lanes sweep rows so accesses stay contiguous
+        const int x = tid % TD;
+        for (int r = tid / TD; r < TD; r += 256 / TD) {
+            if (r0 + r < rows && c0 + x < cols)
+                tile[r * P + x] = src[uint64_t(r0 + r) * cols + c0 + x];
+        }
+        __syncthreads();
+        for (int c = tid / TD; c < TD; c += 256 / TD) {
+            if (c0 + c < cols && r0 + x < rows)
+                dst[uint64_t(c0 + c) * rows + r0 + x] = tile[x * P + c];
+        }
+    }
+}
+
 // ---- dispatch ---------------------------------------------------------------
 
 template<typename F>
@@ -1027,6 +1097,39 @@ launch_tile_frame_sliced(int dtype,
 {
     return launch_tile_impl(dtype, src, W, H, tile_rows, tile_cols, dst, slice_flags,
                             true, stream);
+}
+
+hipError_t
+launch_transpose(int dtype,
+                 const void* src,
+                 uint32_t rows,
+                 uint32_t cols,
+                 void* dst,
+                 hipStream_t stream)
+{
+    if (rows == 0 || cols == 0)
+        return hipErrorInvalidValue;
+    const uint32_t bx = (cols + kTransposeTile - 1) / kTransposeTile;
+    const uint32_t by = (rows + kTransposeTile - 1) / kTransposeTile;
+    if (by > 65535)
+        return hipErrorInvalidValue;
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        // 16-B vectors need 16-B aligned bases and row pitches on both sides
+        const bool vec = (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
+                         (reinterpret_cast<uintptr_t>(dst) % 16) == 0 &&
+                         (uint64_t(cols) * sizeof(T)) % 16 == 0 &&
+                         (uint64_t(rows) * sizeof(T)) % 16 == 0;
+        if (vec)
+            hipLaunchKernelGGL((transpose_kernel<T, true>), dim3(bx, by), dim3(256), 0,
+                               stream, static_cast<const T*>(src), rows, cols,
+                               static_cast<T*>(dst));
+        else
+            hipLaunchKernelGGL((transpose_kernel<T, false>), dim3(bx, by), dim3(256), 0,
+                               stream, static_cast<const T*>(src), rows, cols,
+                               static_cast<T*>(dst));
+        return hipGetLastError();
+    });
 }
 
 hipError_t

@@ -21,11 +21,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -122,6 +125,14 @@ struct aqz_ds
     uint8_t* h_flags = nullptr; // pinned slice flags for on-demand tiling
     size_t h_flags_bytes = 0;
 
+    // aqz_ds_set_input_transpose: input frames arrive in acquisition order
+    // (rows = level-0 width) and are transposed into d_tin on the device
+    bool transpose = false;
+    void* d_tin = nullptr;
+    // the last level-0 frame added (storage order), for aqz_ds_take_input_frame;
+    // null once taken or after a batch
+    const void* last_input = nullptr;
+
     // aqz_ds_run_host_batch pipeline, allocated on first use
     struct Pipe
     {
@@ -131,6 +142,18 @@ struct aqz_ds
         std::vector<void*> d_out[2];         // per level, group-sized
         hipEvent_t in_done[2] = {}, work_done[2] = {}, out_done[2] = {};
     } pipe;
+
+    // aqz_ds_add_frame_async: one worker thread (started on first use) runs
+    // at most one pending add_frame; every other entry point settles it first
+    struct Async
+    {
+        std::thread worker;
+        std::mutex m;
+        std::condition_variable cv;
+        const void* frame = nullptr; // the pending job's frame, null when idle
+        bool stop = false;
+        int rc = 0;                  // status of the last finished job
+    } async;
 
     std::string err;
 
@@ -190,6 +213,55 @@ tile_geom(const aqz_ds* ds, uint32_t L, uint32_t tr, uint32_t tc)
     const size_t ntx = (lv.width + tc - 1) / tc, nty = (lv.height + tr - 1) / tr;
     const size_t nt = ntx * nty;
     return { nt, nt * tr * tc * ds->bpp, nt * aqz::tile_slices(tr, tc) };
+}
+
+// D2H of tiles already laid out on the device, then one flag per tile from
+// its slice flags (pinned, written by the tile kernel).
+int
+tiles_to_host(aqz_ds* ds, const TileGeom& g, const void* d_tiles, const uint8_t* flags,
+              void* dst, uint8_t* tile_nonzero)
+{
+    HIP_TRY(ds,
+            hipMemcpyAsync(dst, d_tiles, g.tile_bytes, hipMemcpyDeviceToHost, ds->stream),
+            "hipMemcpyAsync D2H");
+    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+    if (tile_nonzero) {
+        const size_t slices = g.flag_bytes / g.n_tiles;
+        for (size_t t = 0; t < g.n_tiles; ++t) {
+            uint8_t any = 0;
+            for (size_t q = 0; q < slices; ++q)
+                any |= flags[t * slices + q];
+            tile_nonzero[t] = any ? 1 : 0;
+        }
+    }
+    return AQZ_OK;
+}
+
+// Tile a device frame into the on-demand scratch buffers and copy it out.
+int
+tile_to_host(aqz_ds* ds, const void* d_frame, const aqz_level_desc& lv, uint32_t tile_rows,
+             uint32_t tile_cols, const TileGeom& g, void* dst, uint8_t* tile_nonzero)
+{
+    if (ds->d_tiles_bytes < g.tile_bytes) {
+        (void)hipFree(ds->d_tiles);
+        ds->d_tiles = nullptr;
+        ds->d_tiles_bytes = 0;
+        HIP_TRY(ds, hipMalloc(&ds->d_tiles, g.tile_bytes), "hipMalloc tiles");
+        ds->d_tiles_bytes = g.tile_bytes;
+    }
+    if (ds->h_flags_bytes < g.flag_bytes) {
+        (void)hipHostFree(ds->h_flags);
+        ds->h_flags = nullptr;
+        ds->h_flags_bytes = 0;
+        HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&ds->h_flags), g.flag_bytes,
+                                  hipHostMallocDefault), "hipHostMalloc flags");
+        ds->h_flags_bytes = g.flag_bytes;
+    }
+    HIP_TRY(ds,
+            aqz::launch_tile_frame_sliced(ds->dtype, d_frame, lv.width, lv.height, tile_rows,
+                                          tile_cols, ds->d_tiles, ds->h_flags, ds->stream),
+            "tile kernel");
+    return tiles_to_host(ds, g, ds->d_tiles, ds->h_flags, dst, tile_nonzero);
 }
 
 // Working buffer for a level-L result: the caller's batch slot when the
@@ -363,11 +435,114 @@ bind_device(aqz_ds* ds)
     return AQZ_OK;
 }
 
+int
+check_host_frame(aqz_ds* ds, const void* host_frame, size_t nbytes, const char* who)
+{
+    if (!host_frame || nbytes != ds->bytes[0])
+        return ds->fail_arg(std::string(who) + ": expected " +
+                            std::to_string(ds->bytes[0]) + " bytes, got " +
+                            std::to_string(nbytes));
+    return AQZ_OK;
+}
+
+// The pyramid of one level-0 frame already on the device.  With input
+// transposition the frame is first transposed into storage order
+// (transpose_frame, array.cpp:517-530), which is what the reference's
+// downsampler receives.
+int
+process_input(aqz_ds* ds, const void* d_frame)
+{
+    if (ds->transpose) {
+        // acquisition rows = storage width (array.dimensions.cpp:578-599)
+        HIP_TRY(ds,
+                aqz::launch_transpose(ds->dtype, d_frame, ds->lv[0].width,
+                                      ds->lv[0].height, ds->d_tin, ds->stream),
+                "transpose kernel");
+        d_frame = ds->d_tin;
+    }
+    ds->last_input = d_frame;
+    return process_frame(ds, d_frame, Sink{});
+}
+
+// Downsampler::add_frame for a host frame: upload it, queue the pyramid, and
+// return once the upload has completed (the caller may then reuse its frame;
+// the kernels are still queued).
+int
+add_host_frame(aqz_ds* ds, const void* host_frame)
+{
+    if (int rc = bind_device(ds))
+        return rc;
+    const size_t nbytes = ds->bytes[0];
+    const void* src = host_frame;
+    if (ds->staged) {
+        // previous upload must be done before the staging buffer is reused
+        HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
+        std::memcpy(ds->h_stage, host_frame, nbytes);
+        src = ds->h_stage;
+    }
+    // Straight from the caller's (pageable) frame: the copy engine reads it
+    // at full PCIe rate, no host staging memcpy (tools/e2e_probe.cpp).
+    HIP_TRY(ds,
+            hipMemcpyAsync(ds->d_in, src, nbytes, hipMemcpyHostToDevice, ds->stream),
+            "hipMemcpyAsync H2D");
+    HIP_TRY(ds, hipEventRecord(ds->h2d_done, ds->stream), "hipEventRecord");
+    int rc = process_input(ds, ds->d_in);
+    if (rc)
+        return rc;
+    if (!ds->staged) {
+        // the caller may reuse its frame as soon as we return
+        HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
+    }
+    return AQZ_OK;
+}
+
+void
+async_worker(aqz_ds* ds)
+{
+    auto& a = ds->async;
+    std::unique_lock<std::mutex> lk(a.m);
+    for (;;) {
+        a.cv.wait(lk, [&] { return a.stop || a.frame != nullptr; });
+        if (!a.frame)
+            return; // stop requested and nothing pending
+        const void* frame = a.frame;
+        lk.unlock();
+        const int rc = add_host_frame(ds, frame);
+        lk.lock();
+        a.rc = rc;
+        a.frame = nullptr;
+        a.cv.notify_all();
+    }
+}
+
+// Wait for a pending aqz_ds_add_frame_async; returns (and clears) its status.
+int
+settle(aqz_ds* ds)
+{
+    auto& a = ds->async;
+    if (!a.worker.joinable())
+        return AQZ_OK;
+    std::unique_lock<std::mutex> lk(a.m);
+    a.cv.wait(lk, [&] { return a.frame == nullptr; });
+    const int rc = a.rc;
+    a.rc = AQZ_OK;
+    return rc;
+}
+
 void
 release(aqz_ds* ds)
 {
     if (!ds)
         return;
+    if (ds->async.worker.joinable()) {
+        (void)settle(ds);
+        {
+            std::lock_guard<std::mutex> lk(ds->async.m);
+            ds->async.stop = true;
+        }
+        ds->async.cv.notify_all();
+        ds->async.worker.join();
+    }
     // Best-effort teardown: errors here have nowhere to go.
     (void)hipSetDevice(ds->device);
     if (ds->stream)
@@ -390,6 +565,7 @@ release(aqz_ds* ds)
         (void)hipHostFree(t.second);
     }
     (void)hipHostFree(ds->h_flags);
+    (void)hipFree(ds->d_tin);
     if (ds->h2d_done)
         (void)hipEventDestroy(ds->h2d_done);
     for (int b = 0; b < 2; ++b) {
@@ -597,32 +773,39 @@ aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes)
 {
     if (!ds)
         return AQZ_INVALID_ARGUMENT;
-    if (!host_frame || nbytes != ds->bytes[0])
-        return ds->fail_arg("add_frame: expected " + std::to_string(ds->bytes[0]) +
-                            " bytes, got " + std::to_string(nbytes));
-    if (int rc = bind_device(ds))
+    if (int rc = settle(ds))
         return rc;
-    const void* src = host_frame;
-    if (ds->staged) {
-        // previous upload must be done before the staging buffer is reused
-        HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
-        std::memcpy(ds->h_stage, host_frame, nbytes);
-        src = ds->h_stage;
-    }
-    // Straight from the caller's (pageable) frame: the copy engine reads it
-    // at full PCIe rate, no host staging memcpy (tools/e2e_probe.cpp).
-    HIP_TRY(ds,
-            hipMemcpyAsync(ds->d_in, src, nbytes, hipMemcpyHostToDevice, ds->stream),
-            "hipMemcpyAsync H2D");
-    HIP_TRY(ds, hipEventRecord(ds->h2d_done, ds->stream), "hipEventRecord");
-    int rc = process_frame(ds, ds->d_in, Sink{});
-    if (rc)
+    if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame"))
         return rc;
-    if (!ds->staged) {
-        // the caller may reuse its frame as soon as we return
-        HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
+    return add_host_frame(ds, host_frame);
+}
+
+int
+aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (int rc = settle(ds))
+        return rc;
+    if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame_async"))
+        return rc;
+    auto& a = ds->async;
+    if (!a.worker.joinable())
+        a.worker = std::thread(async_worker, ds);
+    {
+        std::lock_guard<std::mutex> lk(a.m);
+        a.frame = host_frame;
     }
+    a.cv.notify_all();
     return AQZ_OK;
+}
+
+int
+aqz_ds_wait(aqz_ds* ds)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    return settle(ds);
 }
 
 int
@@ -630,13 +813,15 @@ aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes)
 {
     if (!ds)
         return AQZ_INVALID_ARGUMENT;
+    if (int rc = settle(ds))
+        return rc;
     if (!device_frame || nbytes != ds->bytes[0])
         return ds->fail_arg("add_device_frame: expected " +
                             std::to_string(ds->bytes[0]) + " bytes, got " +
                             std::to_string(nbytes));
     if (int rc = bind_device(ds))
         return rc;
-    return process_frame(ds, device_frame, Sink{});
+    return process_input(ds, device_frame);
 }
 
 int
@@ -650,6 +835,8 @@ aqz_ds_take_frame(aqz_ds* ds,
     if (!ds || !has_frame)
         return AQZ_INVALID_ARGUMENT;
     *has_frame = 0;
+    if (int rc = settle(ds))
+        return rc;
     if (level == 0 || level >= ds->n)
         return AQZ_OK; // the reference's map lookup simply misses
     if (ds->cached[level] < 0)
@@ -679,6 +866,8 @@ aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t
 {
     if (!ds)
         return AQZ_INVALID_ARGUMENT;
+    if (int rc = settle(ds))
+        return rc;
     if (level == 0 || level >= ds->n)
         return ds->fail_arg("set_level_tiling: bad level " + std::to_string(level));
     if ((tile_rows == 0) != (tile_cols == 0))
@@ -725,6 +914,8 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
     if (!ds || !has_frame)
         return AQZ_INVALID_ARGUMENT;
     *has_frame = 0;
+    if (int rc = settle(ds))
+        return rc;
     if (tile_rows == 0 || tile_cols == 0)
         return ds->fail_arg("take_frame_tiled: empty tile");
     if (level == 0 || level >= ds->n || ds->cached[level] < 0)
@@ -740,54 +931,107 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
     if (int rc = bind_device(ds))
         return rc;
     const int k = ds->cached[level];
-    const void* tiles = nullptr;
-    const uint8_t* flags = nullptr;
     if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
         ds->tiled_for[level] == k) {
         // tiled when the frame was emitted (aqz_ds_set_level_tiling)
-        tiles = k == 0 ? ds->tslot[level].first : ds->tslot[level].second;
-        flags = k == 0 ? ds->tflags[level].first : ds->tflags[level].second;
-    } else {
-        // on demand, into the scratch buffers
-        if (ds->d_tiles_bytes < g.tile_bytes) {
-            (void)hipFree(ds->d_tiles);
-            ds->d_tiles = nullptr;
-            ds->d_tiles_bytes = 0;
-            HIP_TRY(ds, hipMalloc(&ds->d_tiles, g.tile_bytes), "hipMalloc tiles");
-            ds->d_tiles_bytes = g.tile_bytes;
-        }
-        if (ds->h_flags_bytes < g.flag_bytes) {
-            (void)hipHostFree(ds->h_flags);
-            ds->h_flags = nullptr;
-            ds->h_flags_bytes = 0;
-            HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&ds->h_flags), g.flag_bytes,
-                                      hipHostMallocDefault), "hipHostMalloc flags");
-            ds->h_flags_bytes = g.flag_bytes;
-        }
-        HIP_TRY(ds,
-                aqz::launch_tile_frame_sliced(ds->dtype, ds->slot_ptr(level, k),
-                                              ds->lv[level].width, ds->lv[level].height,
-                                              tile_rows, tile_cols, ds->d_tiles,
-                                              ds->h_flags, ds->stream),
-                "tile kernel");
-        tiles = ds->d_tiles;
-        flags = ds->h_flags;
-    }
-    HIP_TRY(ds,
-            hipMemcpyAsync(dst, tiles, g.tile_bytes, hipMemcpyDeviceToHost, ds->stream),
-            "hipMemcpyAsync D2H");
-    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-    if (tile_nonzero) {
-        const size_t slices = g.flag_bytes / g.n_tiles;
-        for (size_t t = 0; t < g.n_tiles; ++t) {
-            uint8_t any = 0;
-            for (size_t q = 0; q < slices; ++q)
-                any |= flags[t * slices + q];
-            tile_nonzero[t] = any ? 1 : 0;
-        }
+        if (int rc = tiles_to_host(ds, g,
+                                   k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
+                                   k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
+                                   dst, tile_nonzero))
+            return rc;
+    } else if (int rc = tile_to_host(ds, ds->slot_ptr(level, k), ds->lv[level], tile_rows,
+                                     tile_cols, g, dst, tile_nonzero)) {
+        return rc;
     }
     ds->cached[level] = -1;
     ds->tiled_for[level] = -1;
+    return AQZ_OK;
+}
+
+int
+aqz_ds_set_input_transpose(aqz_ds* ds, int transpose)
+{
+    if (!ds)
+        return AQZ_INVALID_ARGUMENT;
+    if (int rc = settle(ds))
+        return rc;
+    if (int rc = bind_device(ds))
+        return rc;
+    if (transpose && !ds->d_tin) {
+        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        HIP_TRY(ds, hipMalloc(&ds->d_tin, ds->bytes[0]), "hipMalloc transposed input");
+        ds->device_bytes += ds->bytes[0];
+    }
+    ds->transpose = transpose != 0;
+    ds->last_input = nullptr;
+    return AQZ_OK;
+}
+
+int
+aqz_ds_take_input_frame(aqz_ds* ds,
+                        uint32_t tile_rows,
+                        uint32_t tile_cols,
+                        void* dst,
+                        size_t cap,
+                        uint8_t* tile_nonzero,
+                        size_t* nbytes,
+                        int* has_frame)
+{
+    if (!ds || !has_frame)
+        return AQZ_INVALID_ARGUMENT;
+    *has_frame = 0;
+    if (int rc = settle(ds))
+        return rc;
+    if ((tile_rows == 0) != (tile_cols == 0))
+        return ds->fail_arg("take_input_frame: tile_rows and tile_cols must both be 0 "
+                            "or both be nonzero");
+    if (!ds->last_input)
+        return AQZ_OK;
+    const bool tiled = tile_rows != 0;
+    const TileGeom g = tiled ? tile_geom(ds, 0, tile_rows, tile_cols)
+                             : TileGeom{ 1, ds->bytes[0], 0 };
+    *has_frame = 1;
+    if (nbytes)
+        *nbytes = g.tile_bytes;
+    if (!dst)
+        return AQZ_OK;
+    if (cap < g.tile_bytes)
+        return ds->fail_arg("take_input_frame: buffer too small");
+    if (int rc = bind_device(ds))
+        return rc;
+    if (tiled) {
+        if (int rc = tile_to_host(ds, ds->last_input, ds->lv[0], tile_rows, tile_cols, g,
+                                  dst, tile_nonzero))
+            return rc;
+    } else {
+        HIP_TRY(ds,
+                hipMemcpyAsync(dst, ds->last_input, g.tile_bytes, hipMemcpyDeviceToHost,
+                               ds->stream),
+                "hipMemcpyAsync D2H");
+        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+    }
+    ds->last_input = nullptr;
+    return AQZ_OK;
+}
+
+int
+aqz_transpose_frame_device(int dtype,
+                           const void* device_src,
+                           uint32_t rows,
+                           uint32_t cols,
+                           void* device_dst,
+                           void* hip_stream)
+{
+    if (!aqz::dtype_valid(dtype) || !device_src || !device_dst || rows == 0 || cols == 0) {
+        set_global_error("transpose_frame_device: invalid argument");
+        return AQZ_INVALID_ARGUMENT;
+    }
+    const hipError_t e = aqz::launch_transpose(dtype, device_src, rows, cols, device_dst,
+                                               static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) {
+        set_global_error("transpose_frame_device: %s", hipGetErrorString(e));
+        return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
+    }
     return AQZ_OK;
 }
 
@@ -827,6 +1071,12 @@ aqz_ds_run_device_batch(aqz_ds* ds,
 {
     if (!ds)
         return AQZ_INVALID_ARGUMENT;
+    if (int rc = settle(ds))
+        return rc;
+    if (ds->transpose)
+        return ds->fail_arg("ds_run_device_batch: input transposition applies to the per-frame path "
+                            "(add_frame / add_device_frame) only");
+    ds->last_input = nullptr;
     if (!device_frames || !device_out_levels)
         return ds->fail_arg("run_device_batch: null buffer");
     for (uint32_t l = 1; l < ds->n; ++l)
@@ -998,6 +1248,12 @@ aqz_ds_run_host_batch(aqz_ds* ds,
 {
     if (!ds)
         return AQZ_INVALID_ARGUMENT;
+    if (int rc = settle(ds))
+        return rc;
+    if (ds->transpose)
+        return ds->fail_arg("ds_run_host_batch: input transposition applies to the per-frame path "
+                            "(add_frame / add_device_frame) only");
+    ds->last_input = nullptr;
     if (!host_frames || !host_out_levels)
         return ds->fail_arg("run_host_batch: null buffer");
     for (uint32_t l = 1; l < ds->n; ++l)

@@ -154,6 +154,76 @@ void aqz_ds_destroy(aqz_ds* ds);
 int aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes);
 
 /*
+ * aqz_ds_add_frame without waiting: validates the size,
+ * hands the frame to the handle's upload thread and returns at once, so the
+ * caller can chunk the same frame into its level-0 array
+ * (`MultiscaleArray::write_frame`, multiscale.array.cpp:57-74, runs
+ * `arrays_[0]->write_frame` before `write_multiscale_frames_`) while it
+ * crosses PCIe and the pyramid is queued.  `host_frame` must stay valid and
+ * unmodified until aqz_ds_wait returns.  Every other call on the handle
+ * (except the size queries and aqz_ds_last_error) waits for the pending frame
+ * first and, if its add failed, returns that status instead of doing its own
+ * work.  At most one frame is pending: a second aqz_ds_add_frame_async waits
+ * for the first.
+ */
+int aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes);
+
+/*
+ * Wait for the frame passed to aqz_ds_add_frame_async to be uploaded and its
+ * pyramid queued; returns that add's status (AQZ_OK if nothing was pending).
+ * After it returns the caller may reuse the frame buffer.
+ */
+int aqz_ds_wait(aqz_ds* ds);
+
+/*
+ * Transposed storage order (`transpose_frame`,
+ * array.cpp:488-504).  When the array's storage_dimension_order swaps Y and X
+ * (`ArrayDimensions::needs_xy_transposition`, array.dimensions.cpp:563-576),
+ * `Array::write_frame_to_chunks_` transposes each level-0 frame before
+ * chunking it (array.cpp:517-530) and, because it replaces the caller's
+ * frame, the downsampler is fed the transposed frame.  With `transpose` = 1
+ * the handle takes frames in ACQUISITION order — `levels[0].width` rows of
+ * `levels[0].height` pixels (acquisition_frame_rows/cols,
+ * array.dimensions.cpp:578-599) — and transposes them on the GPU before the
+ * pyramid, so the level geometry stays in storage order, as the reference
+ * plans it.  Applies to add_frame, add_frame_async and add_device_frame; the
+ * batch entry points return AQZ_INVALID_ARGUMENT while it is set.
+ */
+int aqz_ds_set_input_transpose(aqz_ds* ds, int transpose);
+
+/*
+ * The last level-0 frame added, in storage order (transposed if input
+ * transposition is on), copied to `dst`: chunk-tiled like
+ * aqz_ds_take_frame_tiled when tile_rows/tile_cols are nonzero (the level-0
+ * half of `Array::write_frame_to_chunks_`, array.cpp:507-622, with the zero
+ * scan in `tile_nonzero`), or the plain row-major frame when both are 0.
+ * One-shot: *has_frame = 0 if no frame was added since the last take (or a
+ * batch ran since).  `dst` == NULL reports *nbytes only.  For
+ * aqz_ds_add_device_frame without transposition the caller's device frame
+ * is read, so it must still be valid.
+ */
+int aqz_ds_take_input_frame(aqz_ds* ds,
+                            uint32_t tile_rows,
+                            uint32_t tile_cols,
+                            void* dst,
+                            size_t cap,
+                            uint8_t* tile_nonzero,
+                            size_t* nbytes,
+                            int* has_frame);
+
+/*
+ * `transpose_frame` (array.cpp:488-504) on the device: `device_dst`
+ * (cols x rows) = transpose of `device_src` (rows x cols), both row-major of
+ * `dtype`.  Queued on `hip_stream` (NULL = default stream), not synchronised.
+ */
+int aqz_transpose_frame_device(int dtype,
+                               const void* device_src,
+                               uint32_t rows,
+                               uint32_t cols,
+                               void* device_dst,
+                               void* hip_stream);
+
+/*
  * Same as aqz_ds_add_frame for a frame already resident in device memory
  * (`device_frame` is a device pointer on the handle's device).  The frame
  * must stay valid until the next call on the handle.

@@ -645,3 +645,27 @@ oracle_tile_frame(int dtype,
     }
     return 0;
 }
+
+/*
+ * transpose_frame (array.cpp:488-504): dst[col][row] = src[row][col], one
+ * bytes_per_pixel memcpy per pixel, output src_cols x src_rows.
+ */
+int
+oracle_transpose_frame(int dtype,
+                       const void* src,
+                       uint32_t src_rows,
+                       uint32_t src_cols,
+                       void* dst)
+{
+    const size_t bpp = oracle_bytes_of_type(dtype);
+    if (!bpp || !src || !dst)
+        return -1;
+    for (uint32_t row = 0; row < src_rows; ++row) {
+        for (uint32_t col = 0; col < src_cols; ++col) {
+            const size_t so = ((size_t)row * src_cols + col) * bpp;
+            const size_t d_o = ((size_t)col * src_rows + row) * bpp;
+            memcpy((uint8_t*)dst + d_o, (const uint8_t*)src + so, bpp);
+        }
+    }
+    return 0;
+}

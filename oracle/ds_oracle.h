@@ -102,6 +102,16 @@ int oracle_tile_frame(int dtype,
                       void* dst,
                       uint8_t* nonzero);
 
+/*
+ * transpose_frame (array.cpp:488-504): the src_rows x src_cols row-major frame
+ * transposed into dst (src_cols x src_rows).  Returns 0 / -1.
+ */
+int oracle_transpose_frame(int dtype,
+                           const void* src,
+                           uint32_t src_rows,
+                           uint32_t src_cols,
+                           void* dst);
+
 /* Stateful downsampler: Downsampler::add_frame / take_frame
  * (downsampler.cpp:306-414) over per-level (width, height, planes). */
 typedef struct oracle_ds oracle_ds;

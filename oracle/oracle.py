@@ -64,6 +64,7 @@ def lib():
         L.oracle_ds_add_frame.argtypes = [vp, vp, sz]
         L.oracle_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz)]
         L.oracle_tile_frame.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, vp, vp]
+        L.oracle_transpose_frame.argtypes = [ctypes.c_int, vp, u32, u32, vp]
         L.oracle_ds_level_count.argtypes = [vp, u32]
         L.oracle_ds_level_count.restype = u32
         _lib = L
@@ -196,6 +197,17 @@ def tile_frame(img: np.ndarray, tile_rows: int, tile_cols: int):
     if rc:
         raise ValueError("oracle_tile_frame failed")
     return out, nz.astype(bool)
+
+
+def transpose_frame(img: np.ndarray):
+    """transpose_frame (array.cpp:488-504) of a rows x cols frame."""
+    img = np.ascontiguousarray(img)
+    rows, cols = img.shape
+    out = np.empty((cols, rows), dtype=img.dtype)
+    if lib().oracle_transpose_frame(dtype_code(img.dtype), img.ctypes.data, rows, cols,
+                                    out.ctypes.data):
+        raise ValueError("oracle_transpose_frame failed")
+    return out
 
 
 def cascade_2d(frame: np.ndarray, n_levels: int, method: int):

@@ -550,3 +550,152 @@ def test_eager_tiling_follows_the_cached_frame(aqz, oracle):
     assert np.array_equal(ds.take_frame(2), want1[1])  # plain take of f0
     assert ds.take_frame_tiled(2, 16, 16) is None
     ds.set_level_tiling(1, 0, 0)
+
+
+# ---- §8(f) row 1: aqz_ds_add_frame_async -----------------------------------
+
+@pytest.mark.parametrize("geo_kind", ["2d", "3d"])
+def test_add_frame_async_matches_oracle(aqz, oracle, geo_kind):
+    """add_frame_async + take_frame equals the oracle frame by frame, with
+    the pending add settled by wait() on even frames and implicitly by the
+    next take/add on odd ones."""
+    if geo_kind == "2d":
+        geo = halving_geometry(1000, 601, 4)
+        shape, n = (601, 1000), 6
+    else:
+        geo = [(256, 128, 9), (128, 64, 5), (64, 32, 3), (32, 16, 2)]
+        shape, n = (128, 256), 9
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+    rng = np.random.default_rng(seed_of("async", geo_kind))
+    for i in range(n):
+        f = rng.integers(0, 65536, shape, dtype=np.uint16)
+        ds.add_frame_async(f)
+        if i % 2 == 0:
+            ds.wait()
+        ref.add_frame(f)
+        for L in range(1, len(geo)):
+            a, b = ds.take_frame(L), ref.take_frame(L)
+            assert (a is None) == (b is None), f"frame {i} L{L} readiness"
+            if a is not None:
+                assert_parity(a, b, f"async frame {i} L{L}")
+    # back-to-back asyncs: the second waits for the first
+    f1 = rng.integers(0, 65536, shape, dtype=np.uint16)
+    f2 = rng.integers(0, 65536, shape, dtype=np.uint16)
+    ds.add_frame_async(f1)
+    ds.add_frame_async(f2)
+    ds.wait()
+    ref.add_frame(f1)
+    ref.add_frame(f2)
+    for L in range(1, len(geo)):
+        a, b = ds.take_frame(L), ref.take_frame(L)
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert_parity(a, b, f"back-to-back L{L}")
+    ds.close()
+
+
+def test_add_frame_async_errors(aqz):
+    geo = halving_geometry(64, 64, 2)
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    with pytest.raises(aqz.AqzError):
+        ds.add_frame_async(np.zeros((64, 63), np.uint16))  # size checked up front
+    ds.wait()  # nothing pending: OK
+    ds.add_frame_async(np.ones((64, 64), np.uint16))
+    ds.close()  # destroy settles the pending add
+
+
+# ---- §8(f) row 2: transposed storage order and level-0 take -----------------
+
+TRANSPOSE_SHAPES = [(64, 64), (4096, 4096), (1000, 777), (129, 4100), (1, 5), (5, 1),
+                    (512, 256), (3, 200)]
+
+
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+def test_transpose_frame_device(aqz, oracle, dtype):
+    """aqz_transpose_frame_device equals the transpose_frame restatement
+    (array.cpp:488-504) bit for bit, vector and element paths."""
+    rng = np.random.default_rng(seed_of("transpose", np.dtype(dtype).name))
+    for rows, cols in TRANSPOSE_SHAPES:
+        if np.dtype(dtype).itemsize == 8 and rows * cols > 1 << 22:
+            continue
+        frame = random_frames(rng, dtype, (rows, cols), specials=False)
+        d_src = to_device(frame)
+        d_dst = empty_device(frame.nbytes)
+        aqz.transpose_frame_device(dtype, d_src.data_ptr(), rows, cols, d_dst.data_ptr(),
+                                   launch_stream())
+        got = from_device(d_dst, dtype, (cols, rows))
+        assert_parity(got, oracle.transpose_frame(frame), f"{rows}x{cols}")
+
+
+@pytest.mark.parametrize("case", [
+    # (storage w, h, levels, dtype, tile_rows, tile_cols)
+    (30, 20, 2, np.int32, 15, 10),          # python test_write_transposed_array
+    (1024, 768, 4, np.uint16, 256, 128),
+    (600, 1000, 3, np.float32, 64, 64),
+    (257, 129, 3, np.uint8, 32, 48),
+], ids=lambda c: f"{c[0]}x{c[1]}_{np.dtype(c[3]).name}")
+def test_input_transpose_pyramid_and_level0(aqz, oracle, case):
+    """With input transposition the handle takes acquisition-order frames,
+    transposes them on the GPU, and both the pyramid and the level-0 frame it
+    hands back (raw and chunk-tiled) equal the reference flow: transpose_frame,
+    then the downsampler and write_frame_to_chunks_ on the transposed frame."""
+    w, h, nl, dt, tr, tc = case
+    geo = halving_geometry(w, h, nl)
+    ds = aqz.Downsampler(geo, dt, 1)
+    ds.set_input_transpose(True)
+    ref = oracle.OracleDownsampler(geo, dt, 1)
+    rng = np.random.default_rng(seed_of("tin", w, h))
+    for i in range(3):
+        acq = random_frames(rng, dt, (w, h), specials=False)  # acquisition: w rows
+        acq[: w // 3] = 0
+        stored = oracle.transpose_frame(acq)                 # (h, w) storage order
+        if i == 1:
+            ds.add_frame_async(acq)
+        else:
+            ds.add_frame(acq)
+        ref.add_frame(stored)
+        if i == 0:
+            assert_parity(ds.take_input_frame(), stored, "level 0 raw")
+        else:
+            tiles, nz = ds.take_input_frame(tr, tc)
+            want_t, want_nz = oracle.tile_frame(stored, tr, tc)
+            assert_parity(tiles, want_t, f"level 0 tiles #{i}")
+            assert np.array_equal(nz, want_nz), f"level 0 zero scan #{i}"
+        assert ds.take_input_frame() is None  # one-shot
+        for L in range(1, nl):
+            a, b = ds.take_frame(L), ref.take_frame(L)
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert_parity(a, b, f"transposed #{i} L{L}")
+    ds.close()
+
+
+def test_input_frame_take_and_batch_rules(aqz, oracle):
+    """take_input_frame without transposition returns the frame as added;
+    batches clear it, and are refused while transposition is on."""
+    torch = torch_cuda()
+    geo = halving_geometry(256, 128, 3)
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    rng = np.random.default_rng(5)
+    f = rng.integers(0, 65536, (128, 256), dtype=np.uint16)
+    assert ds.take_input_frame() is None
+    ds.add_frame(f)
+    assert np.array_equal(ds.take_input_frame(), f)
+    d_f = to_device(f)
+    ds.add_device_frame(d_f.data_ptr(), f.nbytes)
+    tiles, nz = ds.take_input_frame(64, 64)
+    assert_parity(tiles, oracle.tile_frame(f, 64, 64)[0], "device input tiles")
+    ds.add_frame(f)
+    bufs = [empty_device(ds.level_bytes(L) * 2) for L in (1, 2)]
+    outs = [0] + [b.data_ptr() for b in bufs]
+    ds.run_device_batch(d_f.data_ptr(), 1, outs)
+    torch.cuda.synchronize()
+    assert ds.take_input_frame() is None
+    ds.set_input_transpose(True)
+    with pytest.raises(aqz.AqzError):
+        ds.run_device_batch(d_f.data_ptr(), 1, outs)
+    with pytest.raises(aqz.AqzError):
+        ds.take_input_frame(16, 0)
+    ds.set_input_transpose(False)
+    ds.close()

@@ -178,3 +178,19 @@ def test_tile_frame_geometry_and_bytes(oracle):
         want = pad.reshape(nty, tr, ntx, tc).transpose(0, 2, 1, 3).reshape(-1, tr, tc)
         np.testing.assert_array_equal(tiles, want)
         assert not nz[0] and nz[1:].all()
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int32, np.float32,
+                                   np.uint64, np.float64],
+                         ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("shape", [(1, 1), (1, 7), (7, 1), (30, 20), (65, 129)])
+def test_oracle_transpose_frame(oracle, dtype, shape):
+    """transpose_frame restatement (array.cpp:488-504) against numpy's
+    transpose, which is what python/tests/test_stream.py::
+    test_write_transposed_array expects the stored array to equal
+    (np.transpose(data, (0, 1, 2, 4, 3)) for a t,c,z,x,y acquisition)."""
+    rng = np.random.default_rng(sum(shape))
+    frame = rng.integers(0, 255, size=shape).astype(dtype)
+    got = oracle.transpose_frame(frame)
+    assert got.shape == shape[::-1]
+    assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(frame.T).view(np.uint8))
