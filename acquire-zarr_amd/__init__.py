@@ -249,8 +249,9 @@ class Downsampler:
                 self._h, 0, 0, out.ctypes.data, out.nbytes, None, ctypes.byref(nb),
                 ctypes.byref(has)))
             return out if has.value else None
-        nt = (-(-h // tile_rows)) * (-(-w // tile_cols))
-        out = np.empty((nt, tile_rows, tile_cols), dtype=self.dtype)
+        # a half-zero tile shape is passed through for the C ABI to reject
+        nt = (-(-h // tile_rows)) * (-(-w // tile_cols)) if tile_rows and tile_cols else 1
+        out = np.empty((nt, max(tile_rows, 1), max(tile_cols, 1)), dtype=self.dtype)
         nz = np.empty(nt, dtype=np.uint8)
         self._check(lib().aqz_ds_take_input_frame(
             self._h, tile_rows, tile_cols, out.ctypes.data, out.nbytes, nz.ctypes.data,
