@@ -314,6 +314,8 @@ def main():
                               tile=(chunk, chunk))
             e2e["pipelined"] = measure_e2e_pipelined(aqz, torch, geo, dtype, method,
                                                      d_in, min(B, 64), device)
+            e2e["secondary_kernels"] = measure_secondary(aqz, torch, stream, d_in, W, H,
+                                                         dtype, chunk)
             if args.sink:
                 e2e["filesystem_sink"] = measure_e2e_sink(aqz, geo, dtype, method,
                                                           args.e2e_frames, device,
@@ -355,6 +357,52 @@ def main():
     ds.close()
     if dist:
         dist.destroy_process_group()
+
+
+def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
+    """§8(f) row-2 kernels on one level-0 frame, timed with HIP events on the
+    launch stream: chunk tiling (aqz_tile_frame_device, chunk x chunk tiles)
+    and transpose_frame (aqz_transpose_frame_device).  Both move
+    2 * frame_bytes algorithmic bytes (read the frame, write it once in the
+    new order; the tiling's overhang is zero for these sizes).  The CPU column
+    times the reference's transpose_frame loop (oracle restatement, 1 core)."""
+    import oracle as orc_mod  # cpu column only
+    bpp = np.dtype(dtype).itemsize
+    fb = W * H * bpp
+    ntx, nty = -(-W // chunk), -(-H // chunk)
+    tiles = torch.empty(ntx * nty * chunk * chunk * bpp, dtype=torch.uint8, device="cuda")
+    nz = torch.empty(ntx * nty, dtype=torch.int32, device="cuda")
+    tout = torch.empty(fb, dtype=torch.uint8, device="cuda")
+    sptr = stream.cuda_stream
+    src = d_in.data_ptr()
+    res = {}
+
+    def timed(name, launch, alg_bytes):
+        for _ in range(3):
+            launch()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            launch()
+            b.record(stream)
+        torch.cuda.synchronize()
+        us = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e3
+        gbs = alg_bytes / (us * 1e-6) / 1e9
+        res[name] = {"avg_launch_us": round(us, 2), "alg_bytes": alg_bytes,
+                     "achieved_GBps": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+    timed("tile_kernel", lambda: aqz.tile_frame_device(
+        dtype, src, W, H, chunk, chunk, tiles.data_ptr(), nz.data_ptr(), sptr),
+        fb + ntx * nty * chunk * chunk * bpp)
+    timed("transpose_kernel", lambda: aqz.transpose_frame_device(
+        dtype, src, H, W, tout.data_ptr(), sptr), 2 * fb)
+    frame = d_in[:fb].cpu().numpy().view(dtype).reshape(H, W)
+    t0 = time.perf_counter()
+    orc_mod.transpose_frame(frame)
+    res["transpose_kernel"]["cpu_reference_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+    return res
 
 
 def measure_traffic(args, kernel):

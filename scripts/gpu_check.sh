@@ -42,6 +42,11 @@ for s in $STEPS; do
     rc=$?; echo "prof rc=$rc"; tail -3 "$OUT/prof.log"
     find "$OUT/prof" -name "*stats*" | head
     [ $rc -eq 0 ] || exit $rc ;;
+  probe)
+    echo "== write_frame probe"
+    timeout -k 10 300 tools/write_frame_probe ${PROBE_ARGS:-} > "$OUT/write_frame_probe.json" 2> "$OUT/write_frame_probe.err"
+    rc=$?; echo "probe rc=$rc"; cat "$OUT/write_frame_probe.json"; tail -3 "$OUT/write_frame_probe.err"
+    [ $rc -eq 0 ] || exit $rc ;;
   pmc)
     echo "== rocprofv3 pmc"
     export TMPDIR=/tmp
