@@ -651,15 +651,15 @@ tile_kernel(const T* __restrict__ src,
     const uint32_t t = blockIdx.x / slices;
     const uint32_t s = blockIdx.x % slices;
     const uint32_t ty = t / n_tiles_x, tx = t % n_tiles_x;
-    const uint64_t tile_elems = uint64_t(tile_rows) * tile_cols;
-    const uint64_t per = (tile_elems + slices - 1) / slices;
-    const uint64_t e0 = uint64_t(s) * per;
-    const uint64_t e1 = e0 + per < tile_elems ? e0 + per : tile_elems;
+    const uint32_t tile_elems = tile_rows * tile_cols; // < 2^31, checked by the launcher
+    const uint32_t per = (tile_elems + slices - 1) / slices;
+    const uint32_t e0 = s * per;
+    const uint32_t e1 = e0 + per < tile_elems ? e0 + per : tile_elems;
     T* out = dst + uint64_t(t) * tile_elems;
     bool any = false;
-    for (uint64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-        const uint32_t r = uint32_t(e / tile_cols);
-        const uint32_t c = uint32_t(e % tile_cols);
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const uint32_t r = e / tile_cols;
+        const uint32_t c = e % tile_cols;
         const uint32_t row = ty * tile_rows + r;
         const uint32_t col = tx * tile_cols + c;
         T v = T(0);
@@ -668,6 +668,71 @@ tile_kernel(const T* __restrict__ src,
             any = any || nonzero_bits(v);
         }
         out[e] = v;
+    }
+    const bool block_any = __syncthreads_or(any);
+    if (threadIdx.x == 0) {
+        if constexpr (SLICE_FLAGS) {
+            static_cast<uint8_t*>(flags)[blockIdx.x] = block_any ? 1 : 0;
+        } else if (block_any) {
+            atomicOr(static_cast<uint32_t*>(flags) + t, 1u);
+        }
+    }
+}
+
+// 16-B vector form for frames whose rows and tiles are 16-B multiples (so a
+// vector is entirely inside or entirely outside the frame): block = one
+// (tile, slice of rows); lane = one 16-B vector of a tile row.
+__device__ __forceinline__ bool
+nonzero_vec(u32x4 v)
+{
+    return (v.x | v.y | v.z | v.w) != 0;
+}
+
+template<bool SLICE_FLAGS>
+__global__ __launch_bounds__(256) void
+tile_kernel_vec(const u32x4* __restrict__ src,
+                uint32_t row_vecs,   // W * bpp / 16
+                uint32_t H,
+                uint32_t tile_rows,
+                uint32_t tile_vecs,  // tile_cols * bpp / 16
+                uint32_t n_tiles_x,
+                uint32_t slices,
+                u32x4* __restrict__ dst,
+                void* __restrict__ flags)
+{
+    const uint32_t t = blockIdx.x / slices;
+    const uint32_t s = blockIdx.x % slices;
+    const uint32_t ty = t / n_tiles_x, tx = t % n_tiles_x;
+    const uint32_t rows_per = (tile_rows + slices - 1) / slices;
+    const uint32_t r0 = s * rows_per;
+    const uint32_t r1 = r0 + rows_per < tile_rows ? r0 + rows_per : tile_rows;
+    // 32-bit in-slice indices (the launcher keeps a tile below 2^31 vectors)
+    const uint32_t n = (r1 > r0 ? r1 - r0 : 0) * tile_vecs;
+    u32x4* out = dst + uint64_t(t) * tile_rows * tile_vecs + uint64_t(r0) * tile_vecs;
+    const uint32_t col_v0 = tx * tile_vecs;
+    bool any = false;
+    // U vectors per lane per round, all loads issued before the stores
+    constexpr uint32_t U = 4;
+    for (uint32_t e0 = threadIdx.x; e0 < n; e0 += U * blockDim.x) {
+        u32x4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t e = e0 + u * blockDim.x;
+            const uint32_t r = r0 + e / tile_vecs;
+            const uint32_t cv = col_v0 + e % tile_vecs;
+            const uint32_t row = ty * tile_rows + r;
+            v[u] = u32x4{ 0u, 0u, 0u, 0u };
+            if (e < n && row < H && cv < row_vecs)
+                v[u] = __builtin_nontemporal_load(src + uint64_t(row) * row_vecs + cv);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t e = e0 + u * blockDim.x;
+            if (e < n) {
+                any = any || nonzero_vec(v[u]);
+                __builtin_nontemporal_store(v[u], out + e);
+            }
+        }
     }
     const bool block_any = __syncthreads_or(any);
     if (threadIdx.x == 0) {
@@ -691,16 +756,18 @@ tile_kernel(const T* __restrict__ src,
 // access on interior tiles.  Edge tiles (and VEC=false frames, whose rows are
 // not 16-B aligned) move one element per access.
 
-constexpr int kTransposeTile = 64;
+// tile edge in elements: 256-B row segments on both sides (128 B for u8)
+template<typename T>
+constexpr int kTransposeTile = sizeof(T) == 1 ? 128 : 256 / int(sizeof(T));
 
 template<typename T>
-constexpr int kTransposePitch = kTransposeTile + (sizeof(T) >= 4 ? 1 : 4 / int(sizeof(T)));
+constexpr int kTransposePitch = kTransposeTile<T> + (sizeof(T) >= 4 ? 1 : 4 / int(sizeof(T)));
 
 template<typename T, bool VEC>
 __global__ __launch_bounds__(256) void
 transpose_kernel(const T* __restrict__ src, uint32_t rows, uint32_t cols, T* __restrict__ dst)
 {
-    constexpr int TD = kTransposeTile;
+    constexpr int TD = kTransposeTile<T>;
     constexpr int P = kTransposePitch<T>;
     __shared__ T tile[TD * P];
     const uint32_t c0 = blockIdx.x * TD; // source columns = destination rows
@@ -1040,7 +1107,8 @@ launch_tile_impl(int dtype,
                  bool slice_flags,
                  hipStream_t stream)
 {
-    if (W == 0 || H == 0 || tile_rows == 0 || tile_cols == 0)
+    if (W == 0 || H == 0 || tile_rows == 0 || tile_cols == 0 ||
+        uint64_t(tile_rows) * tile_cols >= (1ull << 31))
         return hipErrorInvalidValue;
     const uint32_t ntx = (W + tile_cols - 1) / tile_cols;
     const uint32_t nty = (H + tile_rows - 1) / tile_rows;
@@ -1052,6 +1120,22 @@ launch_tile_impl(int dtype,
         hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * ntx * nty, stream);
         if (e != hipSuccess)
             return e;
+    }
+    const size_t bpp = dtype_bytes(dtype);
+    if ((uint64_t(W) * bpp) % 16 == 0 && (uint64_t(tile_cols) * bpp) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(dst) % 16 == 0) {
+        const uint32_t rv = uint32_t(uint64_t(W) * bpp / 16);
+        const uint32_t tv = uint32_t(uint64_t(tile_cols) * bpp / 16);
+        const auto* s16 = static_cast<const u32x4*>(src);
+        auto* d16 = static_cast<u32x4*>(dst);
+        if (slice_flags)
+            hipLaunchKernelGGL((tile_kernel_vec<true>), dim3(uint32_t(blocks)), dim3(256), 0,
+                               stream, s16, rv, H, tile_rows, tv, ntx, slices, d16, flags);
+        else
+            hipLaunchKernelGGL((tile_kernel_vec<false>), dim3(uint32_t(blocks)), dim3(256), 0,
+                               stream, s16, rv, H, tile_rows, tv, ntx, slices, d16, flags);
+        return hipGetLastError();
     }
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);
@@ -1109,12 +1193,13 @@ launch_transpose(int dtype,
 {
     if (rows == 0 || cols == 0)
         return hipErrorInvalidValue;
-    const uint32_t bx = (cols + kTransposeTile - 1) / kTransposeTile;
-    const uint32_t by = (rows + kTransposeTile - 1) / kTransposeTile;
-    if (by > 65535)
-        return hipErrorInvalidValue;
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);
+        constexpr uint32_t TD = kTransposeTile<T>;
+        const uint32_t bx = (cols + TD - 1) / TD;
+        const uint32_t by = (rows + TD - 1) / TD;
+        if (by > 65535)
+            return hipErrorInvalidValue;
         // 16-B vectors need 16-B aligned bases and row pitches on both sides
         const bool vec = (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
                          (reinterpret_cast<uintptr_t>(dst) % 16) == 0 &&

@@ -398,6 +398,8 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
         fb + ntx * nty * chunk * chunk * bpp)
     timed("transpose_kernel", lambda: aqz.transpose_frame_device(
         dtype, src, H, W, tout.data_ptr(), sptr), 2 * fb)
+    # size-matched ceiling: a D2D copy of the same frame (read + write fb)
+    timed("d2d_copy_same_bytes", lambda: tout.copy_(d_in[:fb]), 2 * fb)
     frame = d_in[:fb].cpu().numpy().view(dtype).reshape(H, W)
     t0 = time.perf_counter()
     orc_mod.transpose_frame(frame)
