@@ -37,6 +37,7 @@ EXPORTS = (
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
     "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_set_input_transpose",
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
+    "aqz_blosc_filter_device", "aqz_crc32c_device",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -90,6 +91,8 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_take_input_frame.argtypes = [vp, u32, u32, vp, sz, vp, ctypes.POINTER(sz),
                                           ctypes.POINTER(ctypes.c_int)]
     L.aqz_transpose_frame_device.argtypes = [ctypes.c_int, vp, u32, u32, vp, vp]
+    L.aqz_blosc_filter_device.argtypes = [ctypes.c_int, u32, u32, vp, sz, u32, vp, vp]
+    L.aqz_crc32c_device.argtypes = [vp, sz, sz, u32, vp, vp]
     L.aqz_ds_add_device_frame.argtypes = [vp, vp, sz]
     L.aqz_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz),
                                     ctypes.POINTER(i32)]
@@ -343,6 +346,30 @@ def transpose_frame_device(dtype, device_src: int, rows: int, cols: int,
     rc = L.aqz_transpose_frame_device(dtype_code(dtype), device_src, rows, cols,
                                       device_dst,
                                       ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+
+
+NOSHUFFLE, SHUFFLE, BITSHUFFLE = 0, 1, 2  # aqz_codec.h
+
+
+def blosc_filter_device(shuffle: int, typesize: int, blocksize: int, device_src: int,
+                        nbytes: int, n_buffers: int, device_dst: int, stream: int = 0):
+    """aqz_blosc_filter_device (asynchronous on `stream`)."""
+    L = lib()
+    rc = L.aqz_blosc_filter_device(shuffle, typesize, blocksize, device_src, nbytes,
+                                   n_buffers, device_dst,
+                                   ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+
+
+def crc32c_device(device_data: int, nbytes: int, stride: int, n_buffers: int,
+                  device_crcs: int, stream: int = 0):
+    """aqz_crc32c_device (asynchronous on `stream`)."""
+    L = lib()
+    rc = L.aqz_crc32c_device(device_data, nbytes, stride, n_buffers, device_crcs,
+                             ctypes.c_void_p(stream) if stream else None)
     if rc:
         raise AqzError(rc, L.aqz_last_error().decode())
 

@@ -1,0 +1,465 @@
+// codec_kernels.hip — byte-level codec stages beside the pyramid on gfx950
+// (SURVEY §8(f) rows 3-4), behind include/aqz_codec.h.
+//
+//  * blosc filters: the bytes c-blosc hands its codec for every block of a
+//    chunk buffer (blosc_c's shuffle step; the reference calls
+//    blosc_compress_ctx from compress_in_place, zarr.common.cpp:106-137, on
+//    each chunk, chunk.cpp:78-105).  Byte shuffle gathers byte j of every
+//    element into plane j; bit shuffle (bitshuffle's bshuf_trans_bit_elem)
+//    writes bit row j*8+b = bit b of byte j of every element, LSB first.
+//    Both are pure permutations: HBM-bound, nbytes read + nbytes written.
+//  * crc32c: the Castagnoli CRC of a shard index table (shard.cpp:145-166),
+//    batched over many buffers, one workgroup per buffer.
+//
+// Restated from the published algorithms (c-blosc 1.21 shuffle-generic.c /
+// bitshuffle-generic.c; RFC 3720 CRC-32C); the CPU restatement the tests
+// compare against is oracle/codec_oracle.c.
+#include "codec_kernels.hh"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace aqz {
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// A run of equally sized blocks: block g of the run starts at
+// (g / per) * stride + first + (g % per) * bs.  A launch covers blocks
+// g0 .. g0 + n_blocks - 1 and fewer than 2^31 threads, so thread ids and
+// in-launch divisions stay 32-bit.
+struct BlockRun
+{
+    uint64_t stride; // bytes between buffers
+    uint64_t first;  // offset of the run's first block within a buffer
+    uint32_t per;    // blocks of the run per buffer
+    uint32_t bs;     // block size in bytes
+    uint32_t g0;     // first block of this launch
+};
+
+__device__ __forceinline__ uint64_t
+block_base(const BlockRun& r, uint32_t g)
+{
+    g += r.g0;
+    return uint64_t(g / r.per) * r.stride + r.first + uint64_t(g % r.per) * r.bs;
+}
+
+// 8x8 bit-matrix transpose (bitshuffle's TRANS_BIT_8X8): bit 8r+c -> 8c+r
+__device__ __forceinline__ uint64_t
+trans_bit_8x8(uint64_t x)
+{
+    uint64_t t;
+    t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+    x = x ^ t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+    x = x ^ t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+    x = x ^ t ^ (t << 28);
+    return x;
+}
+
+// ---- byte shuffle -----------------------------------------------------------
+
+// Vector form, TS in {2, 4, 8, 16}: one thread = 8 elements (8*TS bytes in,
+// TS 8-byte stores out, lanes contiguous per plane).  Needs every block of
+// the run to hold a multiple of 8 elements and 16-B aligned block bases.
+template<int TS>
+__global__ __launch_bounds__(256) void
+shuffle_vec_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
+                   uint32_t n_blocks)
+{
+    const uint32_t groups = run.bs / (8 * TS); // 8-element groups per block
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= groups * n_blocks)
+        return;
+    const uint32_t g = gid / groups;
+    const uint32_t q = gid % groups;
+    const uint64_t base = block_base(run, g);
+    const uint32_t ne = run.bs / TS;
+    constexpr int NV = (8 * TS) / 16; // 16-B loads per thread
+    u32x4 v[NV];
+    const auto* s = reinterpret_cast<const u32x4*>(src + base + uint64_t(q) * 8 * TS);
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        v[k] = __builtin_nontemporal_load(s + k);
+    uint8_t e[8 * TS];
+    __builtin_memcpy(e, v, sizeof(e));
+#pragma unroll
+    for (int j = 0; j < TS; ++j) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            w |= uint64_t(e[k * TS + j]) << (8 * k);
+        __builtin_nontemporal_store(
+          w, reinterpret_cast<uint64_t*>(dst + base + uint64_t(j) * ne + uint64_t(q) * 8));
+    }
+}
+
+// Any typesize and block size: one thread per output byte (shuffle_generic).
+__global__ __launch_bounds__(256) void
+shuffle_generic_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
+                       uint32_t n_blocks, uint32_t ts)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= run.bs * n_blocks)
+        return;
+    const uint32_t g = gid / run.bs;
+    const uint32_t o = gid % run.bs;
+    const uint64_t base = block_base(run, g);
+    const uint32_t ne = run.bs / ts;
+    uint8_t v;
+    if (o < ne * ts) {
+        const uint32_t j = o / ne, i = o % ne;
+        v = src[base + uint64_t(i) * ts + j];
+    } else {
+        v = src[base + o]; // blocksize % typesize tail
+    }
+    dst[base + o] = v;
+}
+
+// ---- bit shuffle ------------------------------------------------------------
+
+// Vector form, TS in {1, 2, 4, 8}: one thread = G groups of 8 elements
+// (128 contiguous input bytes); for each of the 8*TS bit rows it writes G
+// bytes.  Needs (elements/8) % G == 0 per block, so row stores stay aligned.
+template<int TS>
+constexpr int kBitGroups = 16 / TS;
+
+template<int TS>
+__global__ __launch_bounds__(256) void
+bitshuffle_vec_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
+                      uint32_t n_blocks)
+{
+    constexpr int G = kBitGroups<TS>;
+    const uint32_t ne = run.bs / TS;
+    const uint32_t row = ne / 8;          // bytes per bit row
+    const uint32_t per_thread = row / G;  // threads per block
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= per_thread * n_blocks)
+        return;
+    const uint32_t g = gid / per_thread;
+    const uint32_t t = gid % per_thread;
+    const uint64_t base = block_base(run, g);
+    u32x4 v[8];
+    const auto* s = reinterpret_cast<const u32x4*>(src + base + uint64_t(t) * 128);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        v[k] = __builtin_nontemporal_load(s + k);
+    uint8_t e[128];
+    __builtin_memcpy(e, v, sizeof(e));
+    // out[r] collects G bytes of bit row r (byte gi = group gi of this thread)
+    uint64_t out[8 * TS][(G + 7) / 8];
+#pragma unroll
+    for (int r = 0; r < 8 * TS; ++r)
+#pragma unroll
+        for (int w = 0; w < (G + 7) / 8; ++w)
+            out[r][w] = 0;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+#pragma unroll
+        for (int j = 0; j < TS; ++j) {
+            uint64_t x = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                x |= uint64_t(e[(gi * 8 + k) * TS + j]) << (8 * k);
+            x = trans_bit_8x8(x);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                out[j * 8 + b][gi / 8] |= ((x >> (8 * b)) & 0xFFull) << (8 * (gi % 8));
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8 * TS; ++r) {
+        uint8_t* d = dst + base + uint64_t(r) * row + uint64_t(t) * G;
+        if constexpr (G == 16) {
+            u32x4 q;
+            __builtin_memcpy(&q, out[r], 16);
+            __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(d));
+        } else if constexpr (G == 8) {
+            __builtin_nontemporal_store(out[r][0], reinterpret_cast<uint64_t*>(d));
+        } else if constexpr (G == 4) {
+            __builtin_nontemporal_store(uint32_t(out[r][0]), reinterpret_cast<uint32_t*>(d));
+        } else {
+            __builtin_nontemporal_store(uint16_t(out[r][0]), reinterpret_cast<uint16_t*>(d));
+        }
+    }
+}
+
+// Any typesize: one thread per output byte.  Blocks whose element count is
+// not a multiple of 8 are copied (c-blosc 1.x bitshuffle()).
+__global__ __launch_bounds__(256) void
+bitshuffle_generic_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
+                          uint32_t n_blocks, uint32_t ts)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= run.bs * n_blocks)
+        return;
+    const uint32_t g = gid / run.bs;
+    const uint32_t o = gid % run.bs;
+    const uint64_t base = block_base(run, g);
+    const uint32_t ne = run.bs / ts;
+    uint8_t v;
+    if (ne % 8 != 0 || o >= ne * ts) {
+        v = src[base + o];
+    } else {
+        const uint32_t row = ne / 8;
+        const uint32_t r = o / row, m = o % row;
+        const uint32_t j = r / 8, b = r % 8;
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < 8; ++k)
+            acc |= ((uint32_t(src[base + uint64_t(8 * m + k) * ts + j]) >> b) & 1u) << k;
+        v = uint8_t(acc);
+    }
+    dst[base + o] = v;
+}
+
+__global__ __launch_bounds__(256) void
+copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
+            uint32_t n_blocks)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= run.bs * n_blocks)
+        return;
+    const uint32_t g = gid / run.bs;
+    const uint32_t o = gid % run.bs;
+    const uint64_t base = block_base(run, g);
+    dst[base + o] = src[base + o];
+}
+
+// Launch one kernel over blocks [g0, g0 + n) of a run; `threads_per_block`
+// threads per data block.
+template<typename L>
+hipError_t
+split_launch(BlockRun run, uint32_t n_blocks, uint64_t threads_per_block, L&& launch)
+{
+    if (threads_per_block == 0)
+        return hipSuccess;
+    const uint64_t cap = (1ull << 31) / threads_per_block; // blocks per launch
+    if (cap == 0)
+        return hipErrorInvalidValue;
+    for (uint64_t g = 0; g < n_blocks; g += cap) {
+        const uint32_t n = uint32_t(n_blocks - g < cap ? n_blocks - g : cap);
+        run.g0 = uint32_t(g);
+        launch(run, n, uint32_t((threads_per_block * n + 255) / 256));
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess)
+            return e;
+    }
+    return hipSuccess;
+}
+
+// One run of equal blocks through the right kernel for `shuffle`.
+hipError_t
+filter_run(int shuffle, uint32_t ts, const uint8_t* src, uint8_t* dst, const BlockRun& run,
+           uint32_t n_blocks, bool aligned, hipStream_t stream)
+{
+    if (n_blocks == 0 || run.bs == 0)
+        return hipSuccess;
+    const uint32_t ne = run.bs / ts;
+    const bool doshuffle = shuffle == 1 && ts > 1;
+    const bool dobit = shuffle == 2 && run.bs >= ts;
+    auto generic = [&](auto kernel) {
+        return split_launch(run, n_blocks, run.bs, [&](BlockRun r, uint32_t n, uint32_t grid) {
+            hipLaunchKernelGGL(kernel, dim3(grid), dim3(256), 0, stream, src, dst, r, n, ts);
+        });
+    };
+    if (doshuffle) {
+        const bool vec = aligned && run.bs % 16 == 0 && run.bs % ts == 0 && ne % 8 == 0 &&
+                         (ts == 2 || ts == 4 || ts == 8 || ts == 16);
+        if (!vec)
+            return generic(shuffle_generic_kernel);
+        return split_launch(run, n_blocks, run.bs / (8 * ts),
+                            [&](BlockRun r, uint32_t n, uint32_t grid) {
+            switch (ts) {
+                case 2:
+                    hipLaunchKernelGGL(shuffle_vec_kernel<2>, dim3(grid), dim3(256), 0, stream,
+                                       src, dst, r, n);
+                    break;
+                case 4:
+                    hipLaunchKernelGGL(shuffle_vec_kernel<4>, dim3(grid), dim3(256), 0, stream,
+                                       src, dst, r, n);
+                    break;
+                case 8:
+                    hipLaunchKernelGGL(shuffle_vec_kernel<8>, dim3(grid), dim3(256), 0, stream,
+                                       src, dst, r, n);
+                    break;
+                default:
+                    hipLaunchKernelGGL(shuffle_vec_kernel<16>, dim3(grid), dim3(256), 0, stream,
+                                       src, dst, r, n);
+                    break;
+            }
+        });
+    }
+    if (dobit) {
+        const int G = (ts == 1 || ts == 2 || ts == 4 || ts == 8) ? int(16 / ts) : 0;
+        const bool vec = aligned && G > 0 && run.bs % ts == 0 && ne % 8 == 0 &&
+                         (ne / 8) % uint32_t(G) == 0 && run.bs % 16 == 0;
+        if (!vec)
+            return generic(bitshuffle_generic_kernel);
+        return split_launch(run, n_blocks, ne / 8 / G,
+                            [&](BlockRun r, uint32_t n, uint32_t grid) {
+            switch (ts) {
+                case 1:
+                    hipLaunchKernelGGL(bitshuffle_vec_kernel<1>, dim3(grid), dim3(256), 0,
+                                       stream, src, dst, r, n);
+                    break;
+                case 2:
+                    hipLaunchKernelGGL(bitshuffle_vec_kernel<2>, dim3(grid), dim3(256), 0,
+                                       stream, src, dst, r, n);
+                    break;
+                case 4:
+                    hipLaunchKernelGGL(bitshuffle_vec_kernel<4>, dim3(grid), dim3(256), 0,
+                                       stream, src, dst, r, n);
+                    break;
+                default:
+                    hipLaunchKernelGGL(bitshuffle_vec_kernel<8>, dim3(grid), dim3(256), 0,
+                                       stream, src, dst, r, n);
+                    break;
+            }
+        });
+    }
+    return split_launch(run, n_blocks, run.bs, [&](BlockRun r, uint32_t n, uint32_t grid) {
+        hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, stream, src, dst, r, n);
+    });
+}
+
+// ---- crc32c -----------------------------------------------------------------
+
+constexpr uint32_t kCrc32cPoly = 0x82F63B78u; // reflected Castagnoli
+
+// a * b mod P over GF(2), reflected bit order (zlib's multmodp)
+__device__ uint32_t
+multmodp(uint32_t a, uint32_t b)
+{
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0)
+                break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ kCrc32cPoly : b >> 1;
+    }
+    return p;
+}
+
+// x^(8n) mod P, from x2n[k] = x^(2^k) mod P
+__device__ uint32_t
+x8nmodp(uint64_t n, const uint32_t* x2n)
+{
+    uint32_t p = 1u << 31; // x^0
+    int k = 3;
+    while (n) {
+        if (n & 1)
+            p = multmodp(x2n[k & 31], p);
+        n >>= 1;
+        ++k;
+    }
+    return p;
+}
+
+// One workgroup per buffer: 256 threads each CRC a contiguous segment with
+// a byte table in LDS, then the segment CRCs are combined left to right
+// (crc(A||B) = crc(A) * x^(8|B|) ^ crc(B), zlib's crc32_combine).
+__global__ __launch_bounds__(256) void
+crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride,
+              uint32_t* __restrict__ crcs)
+{
+    __shared__ uint32_t table[256];
+    __shared__ uint32_t x2n[32];
+    __shared__ uint32_t seg_crc[256];
+    __shared__ uint64_t seg_len[256];
+    const uint32_t tid = threadIdx.x;
+    {
+        uint32_t c = tid;
+        for (int k = 0; k < 8; ++k)
+            c = (c >> 1) ^ (kCrc32cPoly & (0u - (c & 1u)));
+        table[tid] = c;
+    }
+    if (tid == 0) {
+        uint32_t p = 1u << 30; // x^1
+        x2n[0] = p;
+        for (int k = 1; k < 32; ++k)
+            x2n[k] = p = multmodp(p, p);
+    }
+    __syncthreads();
+    const uint8_t* buf = data + uint64_t(blockIdx.x) * stride;
+    const uint64_t per = (nbytes + 255) / 256;
+    const uint64_t b0 = per * tid < nbytes ? per * tid : nbytes;
+    const uint64_t b1 = b0 + per < nbytes ? b0 + per : nbytes;
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = b0; i < b1; ++i)
+        c = (c >> 8) ^ table[(c ^ buf[i]) & 0xFFu];
+    seg_crc[tid] = c ^ 0xFFFFFFFFu; // CRC-32C of the segment alone
+    seg_len[tid] = b1 - b0;
+    __syncthreads();
+    // pairwise tree, left operand keeps the combined CRC and length
+    for (uint32_t s = 1; s < 256; s <<= 1) {
+        if ((tid % (2 * s)) == 0) {
+            const uint32_t r = tid + s;
+            const uint64_t lr = seg_len[r];
+            seg_crc[tid] = lr ? multmodp(x8nmodp(lr, x2n), seg_crc[tid]) ^ seg_crc[r]
+                              : seg_crc[tid];
+            seg_len[tid] += lr;
+        }
+        __syncthreads();
+    }
+    if (tid == 0)
+        crcs[blockIdx.x] = seg_crc[0];
+}
+
+} // namespace
+
+hipError_t
+launch_blosc_filter(int shuffle,
+                    uint32_t typesize,
+                    uint32_t blocksize,
+                    const void* src,
+                    uint64_t nbytes,
+                    uint32_t n_buffers,
+                    void* dst,
+                    hipStream_t stream)
+{
+    if (typesize == 0 || blocksize == 0 || shuffle < 0 || shuffle > 2 || n_buffers == 0)
+        return hipErrorInvalidValue;
+    if (nbytes == 0)
+        return hipSuccess;
+    const auto* s = static_cast<const uint8_t*>(src);
+    auto* d = static_cast<uint8_t*>(dst);
+    const bool aligned = reinterpret_cast<uintptr_t>(s) % 16 == 0 &&
+                         reinterpret_cast<uintptr_t>(d) % 16 == 0 &&
+                         (n_buffers == 1 || nbytes % 16 == 0);
+    const uint64_t full = nbytes / blocksize;
+    const uint32_t leftover = uint32_t(nbytes % blocksize);
+    if (full * n_buffers >= (1ull << 32))
+        return hipErrorInvalidValue;
+    if (full) {
+        const BlockRun run{ nbytes, 0, uint32_t(full), blocksize, 0 };
+        hipError_t e = filter_run(shuffle, typesize, s, d, run, uint32_t(full * n_buffers),
+                                  aligned, stream);
+        if (e != hipSuccess)
+            return e;
+    }
+    if (leftover) {
+        const BlockRun run{ nbytes, full * blocksize, 1, leftover, 0 };
+        return filter_run(shuffle, typesize, s, d, run, n_buffers,
+                          aligned && (full * blocksize) % 16 == 0, stream);
+    }
+    return hipSuccess;
+}
+
+hipError_t
+launch_crc32c(const void* data, uint64_t nbytes, uint64_t stride, uint32_t n_buffers,
+              uint32_t* crcs, hipStream_t stream)
+{
+    if (n_buffers == 0 || n_buffers >= (1u << 31))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(crc32c_kernel, dim3(n_buffers), dim3(256), 0, stream,
+                       static_cast<const uint8_t*>(data), nbytes, stride, crcs);
+    return hipGetLastError();
+}
+
+} // namespace aqz

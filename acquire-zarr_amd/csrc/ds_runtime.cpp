@@ -1425,3 +1425,15 @@ aqz_version(void)
 }
 
 } // extern "C"
+
+namespace aqz {
+
+// aqz_last_error() text for the other C-ABI translation units
+// (codec_runtime.cpp)
+void
+set_last_error(const std::string& msg)
+{
+    g_last_error = msg;
+}
+
+} // namespace aqz

@@ -360,12 +360,14 @@ def main():
 
 
 def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
-    """§8(f) row-2 kernels on one level-0 frame, timed with HIP events on the
-    launch stream: chunk tiling (aqz_tile_frame_device, chunk x chunk tiles)
-    and transpose_frame (aqz_transpose_frame_device).  Both move
-    2 * frame_bytes algorithmic bytes (read the frame, write it once in the
-    new order; the tiling's overhang is zero for these sizes).  The CPU column
-    times the reference's transpose_frame loop (oracle restatement, 1 core)."""
+    """§8(f) kernels on one level-0 frame, timed with HIP events on the
+    launch stream: chunk tiling (aqz_tile_frame_device, chunk x chunk tiles),
+    transpose_frame (aqz_transpose_frame_device), the blosc filters over the
+    frame's chunks and crc32c over index-table-sized buffers.  The tiling,
+    transpose and filters move 2 * frame_bytes algorithmic bytes (read once,
+    write once in the new order; the tiling's overhang is zero at these
+    sizes); crc32c reads its bytes once.  CPU columns time the oracle's
+    restatements on one core (transpose_frame as the reference writes it)."""
     import oracle as orc_mod  # cpu column only
     bpp = np.dtype(dtype).itemsize
     fb = W * H * bpp
@@ -400,6 +402,23 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
         dtype, src, H, W, tout.data_ptr(), sptr), 2 * fb)
     # size-matched ceiling: a D2D copy of the same frame (read + write fb)
     timed("d2d_copy_same_bytes", lambda: tout.copy_(d_in[:fb]), 2 * fb)
+    # §8(f) row 3: blosc filters over the frame as chunk-depth-1 chunks
+    # (chunk x chunk tiles, 64 KiB blocks), one launch for all chunks
+    cbytes = chunk * chunk * bpp
+    nchunks = fb // cbytes
+    for name, mode in (("blosc_shuffle", aqz.SHUFFLE), ("blosc_bitshuffle", aqz.BITSHUFFLE)):
+        timed(name, lambda mode=mode: aqz.blosc_filter_device(
+            mode, bpp, 65536, src, cbytes, nchunks, tout.data_ptr(), sptr), 2 * nchunks * cbytes)
+    # §8(f) row 4: crc32c of 64 shard index tables of 4096 chunks (64 KiB each)
+    crcs = torch.empty(64, dtype=torch.int32, device="cuda")
+    timed("crc32c_64_index_tables", lambda: aqz.crc32c_device(
+        src, 4096 * 16, 4096 * 16 + 4, 64, crcs.data_ptr(), sptr), 64 * 4096 * 16)
+    raw = d_in[:cbytes * 16].cpu().numpy()
+    t0 = time.perf_counter()
+    for k in range(16):
+        orc_mod.blosc_filter(raw[k * cbytes:(k + 1) * cbytes], aqz.BITSHUFFLE, bpp, 65536)
+    res["blosc_bitshuffle"]["cpu_oracle_ms_per_frame"] = round(
+        (time.perf_counter() - t0) * 1e3 * nchunks / 16, 2)
     frame = d_in[:fb].cpu().numpy().view(dtype).reshape(H, W)
     t0 = time.perf_counter()
     orc_mod.transpose_frame(frame)

@@ -65,6 +65,11 @@ def lib():
         L.oracle_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz)]
         L.oracle_tile_frame.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, vp, vp]
         L.oracle_transpose_frame.argtypes = [ctypes.c_int, vp, u32, u32, vp]
+        L.oracle_blosc_filter.argtypes = [ctypes.c_int, u32, u32, vp, sz, vp, vp]
+        L.oracle_blosc_unfilter.argtypes = [ctypes.c_int, u32, u32, vp, sz, vp]
+        L.oracle_crc32c.argtypes = [vp, sz]
+        L.oracle_crc32c.restype = u32
+        L.oracle_shard_index_table.argtypes = [vp, vp, sz, vp]
         L.oracle_ds_level_count.argtypes = [vp, u32]
         L.oracle_ds_level_count.restype = u32
         _lib = L
@@ -207,6 +212,41 @@ def transpose_frame(img: np.ndarray):
     if lib().oracle_transpose_frame(dtype_code(img.dtype), img.ctypes.data, rows, cols,
                                     out.ctypes.data):
         raise ValueError("oracle_transpose_frame failed")
+    return out
+
+
+def blosc_filter(buf, shuffle: int, typesize: int, blocksize: int) -> np.ndarray:
+    """Bytes c-blosc feeds its codec, block by block (codec_oracle.c)."""
+    src = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    out = np.empty_like(src)
+    tmp = np.empty(max(blocksize, 1), np.uint8)
+    if lib().oracle_blosc_filter(shuffle, typesize, blocksize, src.ctypes.data, src.size,
+                                 out.ctypes.data, tmp.ctypes.data):
+        raise ValueError("oracle_blosc_filter: bad arguments")
+    return out
+
+
+def blosc_unfilter(buf, shuffle: int, typesize: int, blocksize: int) -> np.ndarray:
+    src = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    out = np.empty_like(src)
+    if lib().oracle_blosc_unfilter(shuffle, typesize, blocksize, src.ctypes.data, src.size,
+                                   out.ctypes.data):
+        raise ValueError("oracle_blosc_unfilter: bad arguments")
+    return out
+
+
+def crc32c(buf) -> int:
+    b = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    return int(lib().oracle_crc32c(b.ctypes.data, b.size))
+
+
+def shard_index_table(offsets, extents) -> np.ndarray:
+    """Shard::write_table_ (shard.cpp:145-166) bytes: pairs then crc32c."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ext = np.ascontiguousarray(extents, dtype=np.uint64)
+    out = np.empty(16 * off.size + 4, np.uint8)
+    lib().oracle_shard_index_table(off.ctypes.data, ext.ctypes.data, off.size,
+                                   out.ctypes.data)
     return out
 
 

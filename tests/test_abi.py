@@ -15,9 +15,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    src = open(os.path.join(ROOT, "include", "aqz_downsampler.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(aqz_\w+)\s*\(", src)))
+    names = set()
+    inc = os.path.join(ROOT, "include")
+    for h in sorted(os.listdir(inc)):
+        if h.endswith(".h"):
+            src = re.sub(r"/\*.*?\*/", "", open(os.path.join(inc, h)).read(), flags=re.S)
+            names |= set(re.findall(r"\b(aqz_\w+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_header(aqz):
