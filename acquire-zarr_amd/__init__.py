@@ -37,7 +37,8 @@ EXPORTS = (
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
     "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_set_input_transpose",
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
-    "aqz_blosc_filter_device", "aqz_crc32c_device",
+    "aqz_blosc_filter_device", "aqz_crc32c_device", "aqz_tile_slices",
+    "aqz_tile_frame_device_sliced",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
@@ -91,6 +92,9 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_take_input_frame.argtypes = [vp, u32, u32, vp, sz, vp, ctypes.POINTER(sz),
                                           ctypes.POINTER(ctypes.c_int)]
     L.aqz_transpose_frame_device.argtypes = [ctypes.c_int, vp, u32, u32, vp, vp]
+    L.aqz_tile_slices.argtypes = [u32, u32]
+    L.aqz_tile_slices.restype = u32
+    L.aqz_tile_frame_device_sliced.argtypes = [i32, vp, u32, u32, u32, u32, vp, vp, vp]
     L.aqz_blosc_filter_device.argtypes = [ctypes.c_int, u32, u32, vp, sz, u32, vp, vp]
     L.aqz_crc32c_device.argtypes = [vp, sz, sz, u32, vp, vp]
     L.aqz_ds_add_device_frame.argtypes = [vp, vp, sz]
@@ -335,6 +339,23 @@ def tile_frame_device(dtype, device_frame: int, width: int, height: int,
     rc = L.aqz_tile_frame_device(dtype_code(dtype), device_frame, width, height,
                                  tile_rows, tile_cols, device_tiles, device_nonzero,
                                  ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+
+
+def tile_slices(tile_rows: int, tile_cols: int) -> int:
+    return lib().aqz_tile_slices(tile_rows, tile_cols)
+
+
+def tile_frame_device_sliced(dtype, device_frame: int, width: int, height: int,
+                             tile_rows: int, tile_cols: int, device_tiles: int,
+                             device_slice_flags: int, stream: int = 0):
+    """aqz_tile_frame_device_sliced (asynchronous on `stream`)."""
+    L = lib()
+    rc = L.aqz_tile_frame_device_sliced(dtype_code(dtype), device_frame, width, height,
+                                        tile_rows, tile_cols, device_tiles,
+                                        device_slice_flags,
+                                        ctypes.c_void_p(stream) if stream else None)
     if rc:
         raise AqzError(rc, L.aqz_last_error().decode())
 

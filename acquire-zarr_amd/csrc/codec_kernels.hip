@@ -361,15 +361,18 @@ x8nmodp(uint64_t n, const uint32_t* x2n)
     return p;
 }
 
-// One workgroup per buffer: 256 threads each CRC a contiguous segment with
-// a byte table in LDS, then the segment CRCs are combined left to right
-// (crc(A||B) = crc(A) * x^(8|B|) ^ crc(B), zlib's crc32_combine).
+// One workgroup per buffer: 256 threads each CRC a contiguous segment
+// (32 byte loads in flight per thread, slicing-by-8 tables in LDS), then the
+// segment CRCs are combined pairwise left to right,
+// crc(A||B) = crc(A) * x^(8|B|) ^ crc(B) (zlib's crc32_combine), with the
+// per-level powers for full-length right halves computed once.
 __global__ __launch_bounds__(256) void
 crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride,
               uint32_t* __restrict__ crcs)
 {
-    __shared__ uint32_t table[256];
+    __shared__ uint32_t table[8][256];
     __shared__ uint32_t x2n[32];
+    __shared__ uint32_t level_pow[8];
     __shared__ uint32_t seg_crc[256];
     __shared__ uint64_t seg_len[256];
     const uint32_t tid = threadIdx.x;
@@ -377,7 +380,7 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
         uint32_t c = tid;
         for (int k = 0; k < 8; ++k)
             c = (c >> 1) ^ (kCrc32cPoly & (0u - (c & 1u)));
-        table[tid] = c;
+        table[0][tid] = c;
     }
     if (tid == 0) {
         uint32_t p = 1u << 30; // x^1
@@ -386,23 +389,51 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
             x2n[k] = p = multmodp(p, p);
     }
     __syncthreads();
+    for (int k = 1; k < 8; ++k) {
+        const uint32_t prev = table[k - 1][tid];
+        table[k][tid] = (prev >> 8) ^ table[0][prev & 0xFFu];
+    }
+    // segments: 256 of `per` bytes (a multiple of 8), the tail ones shorter
+    const uint64_t per = ((nbytes + 255) / 256 + 7) & ~uint64_t(7);
+    if (tid < 8)
+        level_pow[tid] = x8nmodp(per << tid, x2n);
+    __syncthreads();
     const uint8_t* buf = data + uint64_t(blockIdx.x) * stride;
-    const uint64_t per = (nbytes + 255) / 256;
     const uint64_t b0 = per * tid < nbytes ? per * tid : nbytes;
     const uint64_t b1 = b0 + per < nbytes ? b0 + per : nbytes;
     uint32_t c = 0xFFFFFFFFu;
-    for (uint64_t i = b0; i < b1; ++i)
-        c = (c >> 8) ^ table[(c ^ buf[i]) & 0xFFu];
+    for (uint64_t i = b0; i < b1; i += 32) {
+        uint8_t v[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k)
+            v[k] = i + k < b1 ? buf[i + k] : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (i + 8 * q + 8 <= b1) {
+                const uint8_t* b = v + 8 * q;
+                const uint32_t lo = c ^ (uint32_t(b[0]) | uint32_t(b[1]) << 8 |
+                                         uint32_t(b[2]) << 16 | uint32_t(b[3]) << 24);
+                c = table[7][lo & 0xFFu] ^ table[6][(lo >> 8) & 0xFFu] ^
+                    table[5][(lo >> 16) & 0xFFu] ^ table[4][lo >> 24] ^ table[3][b[4]] ^
+                    table[2][b[5]] ^ table[1][b[6]] ^ table[0][b[7]];
+            } else {
+                for (uint64_t k = i + 8 * q; k < b1 && k < i + 8 * q + 8; ++k)
+                    c = (c >> 8) ^ table[0][(c ^ v[k - i]) & 0xFFu];
+            }
+        }
+    }
     seg_crc[tid] = c ^ 0xFFFFFFFFu; // CRC-32C of the segment alone
     seg_len[tid] = b1 - b0;
     __syncthreads();
-    // pairwise tree, left operand keeps the combined CRC and length
-    for (uint32_t s = 1; s < 256; s <<= 1) {
+    int level = 0;
+    for (uint32_t s = 1; s < 256; s <<= 1, ++level) {
         if ((tid % (2 * s)) == 0) {
             const uint32_t r = tid + s;
             const uint64_t lr = seg_len[r];
-            seg_crc[tid] = lr ? multmodp(x8nmodp(lr, x2n), seg_crc[tid]) ^ seg_crc[r]
-                              : seg_crc[tid];
+            if (lr) {
+                const uint32_t pw = lr == (per << level) ? level_pow[level] : x8nmodp(lr, x2n);
+                seg_crc[tid] = multmodp(pw, seg_crc[tid]) ^ seg_crc[r];
+            }
             seg_len[tid] += lr;
         }
         __syncthreads();

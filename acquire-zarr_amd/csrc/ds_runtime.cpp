@@ -1061,6 +1061,37 @@ aqz_tile_frame_device(int dtype,
     return AQZ_OK;
 }
 
+uint32_t
+aqz_tile_slices(uint32_t tile_rows, uint32_t tile_cols)
+{
+    return aqz::tile_slices(tile_rows, tile_cols);
+}
+
+int
+aqz_tile_frame_device_sliced(int dtype,
+                             const void* device_frame,
+                             uint32_t width,
+                             uint32_t height,
+                             uint32_t tile_rows,
+                             uint32_t tile_cols,
+                             void* device_tiles,
+                             uint8_t* device_slice_flags,
+                             void* hip_stream)
+{
+    if (!aqz::dtype_valid(dtype) || !device_frame || !device_tiles || !device_slice_flags) {
+        set_global_error("tile_frame_device_sliced: invalid argument");
+        return AQZ_INVALID_ARGUMENT;
+    }
+    const hipError_t e = aqz::launch_tile_frame_sliced(
+      dtype, device_frame, width, height, tile_rows, tile_cols, device_tiles,
+      device_slice_flags, static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) {
+        set_global_error("tile_frame_device_sliced: %s", hipGetErrorString(e));
+        return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
+    }
+    return AQZ_OK;
+}
+
 int
 aqz_ds_run_device_batch(aqz_ds* ds,
                         const void* device_frames,

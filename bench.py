@@ -395,7 +395,12 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
                      "achieved_GBps": round(gbs, 1),
                      "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
-    timed("tile_kernel", lambda: aqz.tile_frame_device(
+    slice_flags = torch.empty(ntx * nty * aqz.tile_slices(chunk, chunk), dtype=torch.uint8,
+                              device="cuda")
+    timed("tile_kernel", lambda: aqz.tile_frame_device_sliced(
+        dtype, src, W, H, chunk, chunk, tiles.data_ptr(), slice_flags.data_ptr(), sptr),
+        fb + ntx * nty * chunk * chunk * bpp)
+    timed("tile_kernel_u32_flags_with_memset", lambda: aqz.tile_frame_device(
         dtype, src, W, H, chunk, chunk, tiles.data_ptr(), nz.data_ptr(), sptr),
         fb + ntx * nty * chunk * chunk * bpp)
     timed("transpose_kernel", lambda: aqz.transpose_frame_device(

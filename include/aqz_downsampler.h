@@ -297,6 +297,24 @@ int aqz_tile_frame_device(int dtype,
                           void* hip_stream);
 
 /*
+ * The same tiling with the zero scan split into slices, as the handle's
+ * eager tiling runs it: `device_slice_flags` (device or host-mapped memory)
+ * receives aqz_tile_slices(tile_rows, tile_cols) bytes per tile, tile-major,
+ * each 0 or 1; tile t is nonzero iff any of its slice bytes is.  No
+ * pre-clear and no atomics, so it is a single kernel launch.
+ */
+uint32_t aqz_tile_slices(uint32_t tile_rows, uint32_t tile_cols);
+int aqz_tile_frame_device_sliced(int dtype,
+                                 const void* device_frame,
+                                 uint32_t width,
+                                 uint32_t height,
+                                 uint32_t tile_rows,
+                                 uint32_t tile_cols,
+                                 void* device_tiles,
+                                 uint8_t* device_slice_flags,
+                                 void* hip_stream);
+
+/*
  * Device-resident batch path (benchmark / bulk API).  Equivalent to calling
  * aqz_ds_add_frame on `n_frames` consecutive frames of `device_frames`
  * (frame i at byte offset i*frame_bytes) followed by take_frame on every

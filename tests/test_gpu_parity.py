@@ -465,6 +465,17 @@ def test_tile_frame_device_full_resolution(aqz, oracle):
     assert_parity(from_device(d_tiles, np.uint16, (nt, 256, 256)), tiles, "L0 tiles")
     assert np.array_equal(d_nz.cpu().numpy() != 0, nz)
     assert not nz[0] and not nz[1] and nz[2:].all()
+    # the sliced-flag form (one launch, no pre-clear)
+    sl = aqz.tile_slices(256, 256)
+    d_sl = torch.full((nt * sl,), 7, dtype=torch.uint8, device="cuda")
+    d_tiles.zero_()
+    aqz.tile_frame_device_sliced(np.uint16, d_in.data_ptr(), 4096, 4096, 256, 256,
+                                 d_tiles.data_ptr(), d_sl.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert_parity(from_device(d_tiles, np.uint16, (nt, 256, 256)), tiles, "L0 tiles sliced")
+    flags = d_sl.cpu().numpy().reshape(nt, sl)
+    assert set(np.unique(flags)) <= {0, 1}
+    assert np.array_equal(flags.any(axis=1), nz)
 
 
 @pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32, np.float64],
