@@ -328,79 +328,77 @@ filter_run(int shuffle, uint32_t ts, const uint8_t* src, uint8_t* dst, const Blo
 // ---- crc32c -----------------------------------------------------------------
 
 constexpr uint32_t kCrc32cPoly = 0x82F63B78u; // reflected Castagnoli
+constexpr int kCrcThreads = 1024;
+constexpr int kCrcLevels = 10; // log2(kCrcThreads)
 
-// a * b mod P over GF(2), reflected bit order (zlib's multmodp)
-__device__ uint32_t
+// a * b mod P over GF(2), reflected bit order (zlib's multmodp), branch-free
+__host__ __device__ inline uint32_t
 multmodp(uint32_t a, uint32_t b)
 {
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0)
-                break;
-        }
-        m >>= 1;
-        b = (b & 1) ? (b >> 1) ^ kCrc32cPoly : b >> 1;
+    uint32_t p = 0;
+    for (int k = 31; k >= 0; --k) {
+        p ^= b & (0u - ((a >> k) & 1u));
+        b = (b >> 1) ^ (kCrc32cPoly & (0u - (b & 1u)));
     }
     return p;
 }
 
-// x^(8n) mod P, from x2n[k] = x^(2^k) mod P
-__device__ uint32_t
-x8nmodp(uint64_t n, const uint32_t* x2n)
+// x^(8n) mod P (host side, once per launch)
+uint32_t
+x8nmodp(uint64_t n)
 {
-    uint32_t p = 1u << 31; // x^0
-    int k = 3;
+    uint32_t sq = 1u << 30;   // x^1, squared up to x^(2^k)
+    for (int k = 0; k < 3; ++k)
+        sq = multmodp(sq, sq); // x^8
+    uint32_t p = 1u << 31;    // x^0
     while (n) {
         if (n & 1)
-            p = multmodp(x2n[k & 31], p);
+            p = multmodp(sq, p);
+        sq = multmodp(sq, sq);
         n >>= 1;
-        ++k;
     }
     return p;
 }
 
-// One workgroup per buffer: 256 threads each CRC a contiguous segment
-// (32 byte loads in flight per thread, slicing-by-8 tables in LDS), then the
-// segment CRCs are combined pairwise left to right,
-// crc(A||B) = crc(A) * x^(8|B|) ^ crc(B) (zlib's crc32_combine), with the
-// per-level powers for full-length right halves computed once.
-__global__ __launch_bounds__(256) void
-crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride,
-              uint32_t* __restrict__ crcs)
+struct LevelPow
+{
+    uint32_t v[kCrcLevels]; // x^(8 * per * 2^level) mod P
+};
+
+// One workgroup per buffer.  The buffer is cut into kCrcThreads segments of
+// `per` bytes aligned to its END (the first segments short or empty); each
+// thread CRCs its segment (32 byte loads in flight, slicing-by-8 tables in
+// LDS), then segment CRCs are combined pairwise left to right,
+// crc(A||B) = crc(A) * x^(8|B|) ^ crc(B) (zlib's crc32_combine).  With
+// end-aligned segments a right operand is shorter than s*per only when its
+// left operand is empty (crc 0), so the host-computed per-level powers are
+// the only ones ever needed.
+__global__ __launch_bounds__(kCrcThreads) void
+crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride, uint64_t per,
+              LevelPow pw, uint32_t* __restrict__ crcs)
 {
     __shared__ uint32_t table[8][256];
-    __shared__ uint32_t x2n[32];
-    __shared__ uint32_t level_pow[8];
-    __shared__ uint32_t seg_crc[256];
-    __shared__ uint64_t seg_len[256];
+    __shared__ uint32_t seg_crc[kCrcThreads];
     const uint32_t tid = threadIdx.x;
-    {
+    if (tid < 256) {
         uint32_t c = tid;
         for (int k = 0; k < 8; ++k)
             c = (c >> 1) ^ (kCrc32cPoly & (0u - (c & 1u)));
         table[0][tid] = c;
     }
-    if (tid == 0) {
-        uint32_t p = 1u << 30; // x^1
-        x2n[0] = p;
-        for (int k = 1; k < 32; ++k)
-            x2n[k] = p = multmodp(p, p);
-    }
     __syncthreads();
-    for (int k = 1; k < 8; ++k) {
-        const uint32_t prev = table[k - 1][tid];
-        table[k][tid] = (prev >> 8) ^ table[0][prev & 0xFFu];
+    if (tid < 256) {
+        for (int k = 1; k < 8; ++k) {
+            const uint32_t prev = table[k - 1][tid];
+            table[k][tid] = (prev >> 8) ^ table[0][prev & 0xFFu];
+        }
     }
-    // segments: 256 of `per` bytes (a multiple of 8), the tail ones shorter
-    const uint64_t per = ((nbytes + 255) / 256 + 7) & ~uint64_t(7);
-    if (tid < 8)
-        level_pow[tid] = x8nmodp(per << tid, x2n);
     __syncthreads();
     const uint8_t* buf = data + uint64_t(blockIdx.x) * stride;
-    const uint64_t b0 = per * tid < nbytes ? per * tid : nbytes;
-    const uint64_t b1 = b0 + per < nbytes ? b0 + per : nbytes;
+    const uint64_t from_end0 = per * (kCrcThreads - tid); // start, counted from the end
+    const uint64_t from_end1 = from_end0 - per;
+    const uint64_t b0 = from_end0 < nbytes ? nbytes - from_end0 : 0;
+    const uint64_t b1 = from_end1 < nbytes ? nbytes - from_end1 : 0;
     uint32_t c = 0xFFFFFFFFu;
     for (uint64_t i = b0; i < b1; i += 32) {
         uint8_t v[32];
@@ -422,20 +420,12 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
             }
         }
     }
-    seg_crc[tid] = c ^ 0xFFFFFFFFu; // CRC-32C of the segment alone
-    seg_len[tid] = b1 - b0;
+    seg_crc[tid] = c ^ 0xFFFFFFFFu; // CRC-32C of the segment alone (0 if empty)
     __syncthreads();
     int level = 0;
-    for (uint32_t s = 1; s < 256; s <<= 1, ++level) {
-        if ((tid % (2 * s)) == 0) {
-            const uint32_t r = tid + s;
-            const uint64_t lr = seg_len[r];
-            if (lr) {
-                const uint32_t pw = lr == (per << level) ? level_pow[level] : x8nmodp(lr, x2n);
-                seg_crc[tid] = multmodp(pw, seg_crc[tid]) ^ seg_crc[r];
-            }
-            seg_len[tid] += lr;
-        }
+    for (uint32_t s = 1; s < kCrcThreads; s <<= 1, ++level) {
+        if ((tid % (2 * s)) == 0)
+            seg_crc[tid] = multmodp(pw.v[level], seg_crc[tid]) ^ seg_crc[tid + s];
         __syncthreads();
     }
     if (tid == 0)
@@ -488,8 +478,13 @@ launch_crc32c(const void* data, uint64_t nbytes, uint64_t stride, uint32_t n_buf
 {
     if (n_buffers == 0 || n_buffers >= (1u << 31))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(crc32c_kernel, dim3(n_buffers), dim3(256), 0, stream,
-                       static_cast<const uint8_t*>(data), nbytes, stride, crcs);
+    const uint64_t per = ((nbytes + kCrcThreads - 1) / kCrcThreads + 7) & ~uint64_t(7);
+    LevelPow pw;
+    pw.v[0] = x8nmodp(per);
+    for (int l = 1; l < kCrcLevels; ++l)
+        pw.v[l] = multmodp(pw.v[l - 1], pw.v[l - 1]); // x^(8*per*2^l)
+    hipLaunchKernelGGL(crc32c_kernel, dim3(n_buffers), dim3(kCrcThreads), 0, stream,
+                       static_cast<const uint8_t*>(data), nbytes, stride, per, pw, crcs);
     return hipGetLastError();
 }
 
