@@ -400,26 +400,33 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
     const uint64_t b0 = from_end0 < nbytes ? nbytes - from_end0 : 0;
     const uint64_t b1 = from_end1 < nbytes ? nbytes - from_end1 : 0;
     uint32_t c = 0xFFFFFFFFu;
-    for (uint64_t i = b0; i < b1; i += 32) {
+    auto step8 = [&](const uint8_t* b) { // slicing-by-8
+        const uint32_t lo = c ^ (uint32_t(b[0]) | uint32_t(b[1]) << 8 | uint32_t(b[2]) << 16 |
+                                 uint32_t(b[3]) << 24);
+        c = table[7][lo & 0xFFu] ^ table[6][(lo >> 8) & 0xFFu] ^ table[5][(lo >> 16) & 0xFFu] ^
+            table[4][lo >> 24] ^ table[3][b[4]] ^ table[2][b[5]] ^ table[1][b[6]] ^
+            table[0][b[7]];
+    };
+    uint64_t i = b0;
+    // whole 32-byte runs: 32 unconditional loads in flight, then 4 steps
+    for (; i + 32 <= b1; i += 32) {
         uint8_t v[32];
 #pragma unroll
         for (int k = 0; k < 32; ++k)
-            v[k] = i + k < b1 ? buf[i + k] : 0;
+            v[k] = buf[i + k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (i + 8 * q + 8 <= b1) {
-                const uint8_t* b = v + 8 * q;
-                const uint32_t lo = c ^ (uint32_t(b[0]) | uint32_t(b[1]) << 8 |
-                                         uint32_t(b[2]) << 16 | uint32_t(b[3]) << 24);
-                c = table[7][lo & 0xFFu] ^ table[6][(lo >> 8) & 0xFFu] ^
-                    table[5][(lo >> 16) & 0xFFu] ^ table[4][lo >> 24] ^ table[3][b[4]] ^
-                    table[2][b[5]] ^ table[1][b[6]] ^ table[0][b[7]];
-            } else {
-                for (uint64_t k = i + 8 * q; k < b1 && k < i + 8 * q + 8; ++k)
-                    c = (c >> 8) ^ table[0][(c ^ v[k - i]) & 0xFFu];
-            }
-        }
+        for (int q = 0; q < 4; ++q)
+            step8(v + 8 * q);
     }
+    for (; i + 8 <= b1; i += 8) {
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v[k] = buf[i + k];
+        step8(v);
+    }
+    for (; i < b1; ++i)
+        c = (c >> 8) ^ table[0][(c ^ buf[i]) & 0xFFu];
     seg_crc[tid] = c ^ 0xFFFFFFFFu; // CRC-32C of the segment alone (0 if empty)
     __syncthreads();
     int level = 0;
