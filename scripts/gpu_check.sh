@@ -42,6 +42,15 @@ for s in $STEPS; do
     rc=$?; echo "prof rc=$rc"; tail -3 "$OUT/prof.log"
     find "$OUT/prof" -name "*stats*" | head
     [ $rc -eq 0 ] || exit $rc ;;
+  prof2)
+    echo "== rocprofv3 kernel-trace, 8(f) kernels"
+    export TMPDIR=/tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$OUT/prof2" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 \
+      --cpu-seconds 0 --e2e-frames 8 --no-pmc --no-check > "$OUT/prof2.log" 2>&1
+    rc=$?; echo "prof2 rc=$rc"; tail -3 "$OUT/prof2.log"
+    find "$OUT/prof2" -name "*stats*" | head
+    [ $rc -eq 0 ] || exit $rc ;;
   probe)
     echo "== write_frame probe"
     timeout -k 10 300 tools/write_frame_probe ${PROBE_ARGS:-} > "$OUT/write_frame_probe.json" 2> "$OUT/write_frame_probe.err"
