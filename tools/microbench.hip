@@ -74,6 +74,34 @@ read_kernel(const u32x4* p, uint64_t n, uint32_t* sink)
         sink[0] = acc;
 }
 
+// the same streaming read through LDS-DMA (global_load_lds_dwordx4): each
+// wave lands 8 x 1 KiB per round in its own LDS slots, waits, and touches
+// one dword per slot.  AUX = 2 is the nt policy.
+template<int AUX>
+__global__ __launch_bounds__(256) void
+read_glds_kernel(const u32x4* p, uint64_t n, uint32_t* sink)
+{
+    __shared__ u32x4 buf[4][8][64];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    uint32_t acc = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+    for (; i + 7 * stride < n; i += 8 * stride) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(p + i + k * stride),
+              (__attribute__((address_space(3))) void*)(&buf[w][k][0]), 16, 0, AUX);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            acc ^= buf[w][k][lane].x;
+    }
+    if (acc == 0x12345678u)
+        sink[0] = acc;
+}
+
 // read 3 vectors, write one (their xor), like the cascade's 3:1 byte mix
 __global__ __launch_bounds__(256) void
 r3w1_kernel(const u32x4* p, uint64_t n_out, u32x4* out)
@@ -548,6 +576,16 @@ main(int argc, char** argv)
     std::vector<Variant> vs;
     vs.push_back({ "read (2 GiB, nt)", in_bytes, [&] {
                       hipLaunchKernelGGL(read_kernel, dim3(4096), dim3(256), 0, 0,
+                                         reinterpret_cast<const u32x4*>(d_in),
+                                         in_bytes / 16, sink);
+                  }, false, {} });
+    vs.push_back({ "read (2 GiB, glds nt)", in_bytes, [&] {
+                      hipLaunchKernelGGL(read_glds_kernel<2>, dim3(4096), dim3(256), 0, 0,
+                                         reinterpret_cast<const u32x4*>(d_in),
+                                         in_bytes / 16, sink);
+                  }, false, {} });
+    vs.push_back({ "read (2 GiB, glds default)", in_bytes, [&] {
+                      hipLaunchKernelGGL(read_glds_kernel<0>, dim3(4096), dim3(256), 0, 0,
                                          reinterpret_cast<const u32x4*>(d_in),
                                          in_bytes / 16, sink);
                   }, false, {} });
