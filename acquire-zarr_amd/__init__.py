@@ -276,7 +276,8 @@ class Downsampler:
         return list(counts)
 
     def last_batch_kind(self) -> int:
-        """0 per-frame, 1 fused 2-D cascade, 2 fused volume, -1 none."""
+        """0 per-frame, 1 fused 2-D cascade, 2 fused volume, 3 2-D batch with
+        some runs on batched single-level kernels, -1 none."""
         return lib().aqz_ds_last_batch_kind(self._h)
 
     def device_memory_usage(self) -> int:

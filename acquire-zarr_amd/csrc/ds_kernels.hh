@@ -39,8 +39,17 @@ bool method_valid(int method);
 // True when the fused vector cascade can run the given run of levels: the
 // input width must be a multiple of the per-lane vector (16 bytes of T), all
 // pointers 16-byte aligned and each output level exactly ceil(in/2).
+// Columns per lane the fused cascade would use for this run (0: unsupported).
+uint32_t cascade_pick_cols(int dtype,
+                           const void* src,
+                           uint64_t src_frame_elems,
+                           uint32_t W,
+                           uint32_t H,
+                           const LevelOut* outs,
+                           int n_out);
 bool cascade_supported(int dtype,
                        const void* src,
+                       uint64_t src_frame_elems,
                        uint32_t W,
                        uint32_t H,
                        const LevelOut* outs,

@@ -330,25 +330,30 @@ cascade_unit(const CascadeParams& p,
              int lane)
 {
     constexpr int R = 1 << NL;
-    constexpr int V = C * int(sizeof(T)) / 16; // 16-byte loads per row
+    constexpr int RB = C * int(sizeof(T));   // bytes per lane per row
+    constexpr int LB = RB >= 16 ? 16 : RB;   // bytes per load (8 for narrow tiles)
+    constexpr int V = RB / LB;               // loads per row
+    constexpr int E = LB / int(sizeof(T));   // elements per load
+    static_assert(LB == 16 || LB == 8, "cascade loads are 8 or 16 bytes");
+    using LoadT = std::conditional_t<LB == 16, u32x4, uint64_t>;
     const T* src =
       reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
 
     T v[R][C];
     // All row loads are issued before any arithmetic: 2^NL * V outstanding
-    // 16-byte loads per lane (1 KiB per wave instruction).
+    // loads per lane (1 KiB per wave instruction at 16 B).
 #pragma unroll
     for (int r = 0; r < R; ++r) {
 #pragma unroll
         for (int k = 0; k < V; ++k) {
-            const uint32_t col = col0 + uint32_t(k) * (16 / sizeof(T));
+            const uint32_t col = col0 + uint32_t(k) * E;
             bool ok = true;
             if constexpr (EDGE) {
                 ok = (row0 + r < p.H) && (col < p.W);
             }
-            u32x4 q = { 0u, 0u, 0u, 0u };
+            LoadT q{};
             if (ok) {
-                const u32x4* a = reinterpret_cast<const u32x4*>(
+                const LoadT* a = reinterpret_cast<const LoadT*>(
                   src + uint64_t(row0 + r) * p.W + col);
                 if constexpr (NT) {
                     q = __builtin_nontemporal_load(a);
@@ -356,7 +361,7 @@ cascade_unit(const CascadeParams& p,
                     q = *a;
                 }
             }
-            __builtin_memcpy(&v[r][k * (16 / sizeof(T))], &q, 16);
+            __builtin_memcpy(&v[r][k * E], &q, LB);
         }
     }
     cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS>(p, v, f, row0, col0, lane);
@@ -922,21 +927,27 @@ set_cascade_grid_cap(uint32_t blocks)
     g_cascade_grid_cap = blocks;
 }
 
+namespace {
+
+// Can the fused cascade run this level run with C columns per lane?
 bool
-cascade_supported(int dtype,
-                  const void* src,
-                  uint32_t W,
-                  uint32_t H,
-                  const LevelOut* outs,
-                  int n_out)
+cascade_fits(size_t b,
+             const void* src,
+             uint64_t src_frame_elems,
+             uint32_t W,
+             uint32_t H,
+             const LevelOut* outs,
+             int n_out,
+             uint32_t C)
 {
-    const size_t b = dtype_bytes(dtype);
-    if (!b || n_out < 1 || n_out > kMaxFusedLevels || W == 0 || H == 0)
+    if (!b || C == 0 || n_out < 1 || n_out > kMaxFusedLevels || W == 0 || H == 0)
         return false;
-    // whole 16-byte loads per lane, and a lane never straddles the row end
-    // (stores of a lane's level-J block must stay inside the row)
-    const uint32_t C = cascade_cols(b);
-    if (W % C != 0 || reinterpret_cast<uintptr_t>(src) % 16 != 0)
+    // whole loads per lane (16 B, or 8 B for narrow tiles) from every source
+    // frame of the batch, and a lane never straddles the row end (stores of a
+    // lane's level-J block must stay inside the row)
+    const size_t lb = std::min<size_t>(16, size_t(C) * b);
+    if (W % C != 0 || reinterpret_cast<uintptr_t>(src) % lb != 0 ||
+        (src_frame_elems * b) % lb != 0)
         return false;
     uint32_t w = W, h = H;
     for (int i = 0; i < n_out; ++i) {
@@ -955,6 +966,46 @@ cascade_supported(int dtype,
     return true;
 }
 
+} // namespace
+
+uint32_t
+cascade_pick_cols(int dtype,
+                  const void* src,
+                  uint64_t src_frame_elems,
+                  uint32_t W,
+                  uint32_t H,
+                  const LevelOut* outs,
+                  int n_out)
+{
+    const size_t b = dtype_bytes(dtype);
+    if (!b)
+        return 0;
+    // wide tiles (kCascadeCols) where a wave's 64 lanes fit in the frame;
+    // half-width tiles for narrower frames (a 512-px u8 frame would leave half
+    // of every wide wave idle on the edge path) and for widths only the
+    // narrow tile divides
+    const uint32_t cw = cascade_cols(b), cn = cw / 2;
+    const bool wide = cascade_fits(b, src, src_frame_elems, W, H, outs, n_out, cw);
+    const bool narrow = cascade_fits(b, src, src_frame_elems, W, H, outs, n_out, cn);
+    if (wide && W >= 64 * cw)
+        return cw;
+    if (narrow)
+        return cn;
+    return wide ? cw : 0;
+}
+
+bool
+cascade_supported(int dtype,
+                  const void* src,
+                  uint64_t src_frame_elems,
+                  uint32_t W,
+                  uint32_t H,
+                  const LevelOut* outs,
+                  int n_out)
+{
+    return cascade_pick_cols(dtype, src, src_frame_elems, W, H, outs, n_out) != 0;
+}
+
 hipError_t
 launch_cascade(int dtype,
                int method,
@@ -967,20 +1018,20 @@ launch_cascade(int dtype,
                uint32_t n_frames,
                hipStream_t stream)
 {
-    if (!cascade_supported(dtype, src, W, H, outs, n_out) || n_frames == 0)
-        return hipErrorInvalidValue;
-    if ((src_frame_elems * dtype_bytes(dtype)) % 16 != 0)
+    const uint32_t cols = cascade_pick_cols(dtype, src, src_frame_elems, W, H, outs, n_out);
+    if (cols == 0 || n_frames == 0)
         return hipErrorInvalidValue;
 
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);
-        constexpr uint32_t C = kCascadeCols<T>;
+        constexpr uint32_t CW = kCascadeCols<T>;
+        constexpr uint32_t CN = CW / 2;
         CascadeParams p{};
         p.src = static_cast<const uint8_t*>(src);
         p.src_frame_elems = src_frame_elems;
         p.W = W;
         p.H = H;
-        p.units_x = (W + 64 * C - 1) / (64 * C);
+        p.units_x = (W + 64 * cols - 1) / (64 * cols);
         const uint32_t R = 1u << n_out;
         p.units_y = (H + R - 1) / R;
         const uint64_t total = uint64_t(p.units_x) * p.units_y * n_frames;
@@ -997,24 +1048,31 @@ launch_cascade(int dtype,
         const uint32_t grid = grid_for(total, 4, g_cascade_grid_cap);
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            switch (n_out) {
-                case 1:
-                    hipLaunchKernelGGL((cascade_kernel<T, M, 1>),
-                                       dim3(grid), dim3(256), 0, stream, p);
-                    break;
-                case 2:
-                    hipLaunchKernelGGL((cascade_kernel<T, M, 2>),
-                                       dim3(grid), dim3(256), 0, stream, p);
-                    break;
-                case 3:
-                    hipLaunchKernelGGL((cascade_kernel<T, M, 3>),
-                                       dim3(grid), dim3(256), 0, stream, p);
-                    break;
-                default:
-                    hipLaunchKernelGGL((cascade_kernel<T, M, 4>),
-                                       dim3(grid), dim3(256), 0, stream, p);
-                    break;
-            }
+            auto go = [&](auto ctag) {
+                constexpr int C = decltype(ctag)::value;
+                switch (n_out) {
+                    case 1:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
+                        break;
+                    case 2:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
+                        break;
+                    case 3:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
+                        break;
+                    default:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
+                        break;
+                }
+            };
+            if (cols == CW)
+                go(std::integral_constant<int, int(CW)>{});
+            else
+                go(std::integral_constant<int, int(CN)>{});
             return hipGetLastError();
         });
     });
@@ -1029,7 +1087,8 @@ volume_supported(int dtype,
                  int n_out)
 {
     return n_out >= 1 && n_out <= kMaxVolumeLevels &&
-           cascade_supported(dtype, src, W, H, outs, n_out);
+           cascade_fits(dtype_bytes(dtype), src, uint64_t(W) * H, W, H, outs, n_out,
+                        cascade_cols(dtype_bytes(dtype)));
 }
 
 hipError_t

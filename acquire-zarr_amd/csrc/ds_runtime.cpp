@@ -319,7 +319,7 @@ reduce_xy(aqz_ds* ds, uint32_t L, const void* src, void* dst)
     const aqz_level_desc& a = ds->lv[L - 1];
     aqz::LevelOut o{ dst, elems(ds, L), ds->lv[L].width, ds->lv[L].height };
     hipError_t e;
-    if (aqz::cascade_supported(ds->dtype, src, a.width, a.height, &o, 1))
+    if (aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width, a.height, &o, 1))
         e = aqz::launch_cascade(ds->dtype, ds->method, src, elems(ds, L - 1),
                                 a.width, a.height, &o, 1, 1, ds->stream);
     else
@@ -349,8 +349,8 @@ process_frame(aqz_ds* ds, const void* d_frame, const Sink& sink)
                 outs[j] = { level_target(ds, L + j, sink), elems(ds, L + j),
                             ds->lv[L + j].width, ds->lv[L + j].height };
             const aqz_level_desc& a = ds->lv[L - 1];
-            if (aqz::cascade_supported(ds->dtype, cur, a.width, a.height, outs,
-                                       int(k))) {
+            if (aqz::cascade_supported(ds->dtype, cur, elems(ds, L - 1), a.width, a.height,
+                                       outs, int(k))) {
                 HIP_TRY(ds,
                         aqz::launch_cascade(ds->dtype, ds->method, cur,
                                             elems(ds, L - 1), a.width, a.height,
@@ -1135,10 +1135,17 @@ aqz_ds_run_device_batch(aqz_ds* ds,
     }
     pure_xyz = pure_xyz && n_frames > 0 && (n_frames % (1u << (ds->n - 1))) == 0;
 
-    // Plan fused runs (up to `maxk` levels per launch) and check that every
-    // run can take the vector path before launching anything.
+    // Plan runs of up to `maxk` levels per launch.  A 2-D batch always stays
+    // batched: a run the fused cascade cannot take (width or alignment) runs
+    // as one batched single-level generic launch per level.  A volume batch
+    // is all-or-nothing (its fallback is the per-frame state machine).
+    struct Run
+    {
+        uint32_t L, k;
+        bool fused;
+    };
     auto plan_runs = [&](uint32_t maxk, bool volume) {
-        std::vector<std::pair<uint32_t, uint32_t>> runs; // (first level, count)
+        std::vector<Run> runs;
         const void* src = device_frames;
         for (uint32_t L = 1; L < ds->n;) {
             const uint32_t k = std::min<uint32_t>(ds->n - L, maxk);
@@ -1149,17 +1156,18 @@ aqz_ds_run_device_batch(aqz_ds* ds,
             const aqz_level_desc& a = ds->lv[L - 1];
             const bool ok =
               volume ? aqz::volume_supported(ds->dtype, src, a.width, a.height, o, int(k))
-                     : aqz::cascade_supported(ds->dtype, src, a.width, a.height, o, int(k));
-            if (!ok)
-                return std::vector<std::pair<uint32_t, uint32_t>>{};
-            runs.emplace_back(L, k);
+                     : aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width,
+                                              a.height, o, int(k));
+            if (!ok && volume)
+                return std::vector<Run>{};
+            runs.push_back({ L, k, ok });
             src = o[k - 1].ptr;
             L += k;
         }
         return runs;
     };
 
-    std::vector<std::pair<uint32_t, uint32_t>> runs;
+    std::vector<Run> runs;
     bool volume = false;
     if (pure_xy && n_frames > 0) {
         runs = plan_runs(aqz::kMaxFusedLevels, false);
@@ -1169,35 +1177,48 @@ aqz_ds_run_device_batch(aqz_ds* ds,
     }
 
     if (!runs.empty()) {
-        // Whole batch in fused launches; every frame / plane group independent.
+        // Whole batch in batched launches; every frame / plane group independent.
         const void* src = device_frames;
         uint32_t planes = n_frames;
-        for (const auto& [L, k] : runs) {
+        bool all_fused = true;
+        for (const Run& run : runs) {
             aqz::LevelOut o[aqz::kMaxFusedLevels];
-            for (uint32_t j = 0; j < k; ++j)
-                o[j] = { device_out_levels[L + j], elems(ds, L + j),
-                         ds->lv[L + j].width, ds->lv[L + j].height };
-            const aqz_level_desc& a = ds->lv[L - 1];
-            const hipError_t e =
-              volume ? aqz::launch_volume(ds->dtype, ds->method, src,
-                                          elems(ds, L - 1), a.width, a.height, o,
-                                          int(k), planes, ds->stream)
-                     : aqz::launch_cascade(ds->dtype, ds->method, src,
-                                           elems(ds, L - 1), a.width, a.height, o,
-                                           int(k), n_frames, ds->stream);
+            for (uint32_t j = 0; j < run.k; ++j)
+                o[j] = { device_out_levels[run.L + j], elems(ds, run.L + j),
+                         ds->lv[run.L + j].width, ds->lv[run.L + j].height };
+            const aqz_level_desc& a = ds->lv[run.L - 1];
+            hipError_t e = hipSuccess;
+            if (volume) {
+                e = aqz::launch_volume(ds->dtype, ds->method, src, elems(ds, run.L - 1),
+                                       a.width, a.height, o, int(run.k), planes, ds->stream);
+            } else if (run.fused) {
+                e = aqz::launch_cascade(ds->dtype, ds->method, src, elems(ds, run.L - 1),
+                                        a.width, a.height, o, int(run.k), n_frames,
+                                        ds->stream);
+            } else {
+                all_fused = false;
+                const void* s = src;
+                for (uint32_t j = 0; j < run.k && e == hipSuccess; ++j) {
+                    const aqz_level_desc& in = ds->lv[run.L + j - 1];
+                    e = aqz::launch_xy_generic(ds->dtype, ds->method, s,
+                                               elems(ds, run.L + j - 1), in.width, in.height,
+                                               o[j], n_frames, ds->stream);
+                    s = o[j].ptr;
+                }
+            }
             if (e != hipSuccess) {
                 rc = ds->fail(e, volume ? "batch volume" : "batch cascade");
                 break;
             }
-            src = o[k - 1].ptr;
+            src = o[run.k - 1].ptr;
             if (volume)
-                planes >>= k;
+                planes >>= run.k;
         }
         for (uint32_t l = 0; l < ds->n; ++l) {
             emitted[l] = volume ? (n_frames >> l) : n_frames;
             ds->count[l] += emitted[l];
         }
-        ds->last_batch_kind = volume ? 2 : 1;
+        ds->last_batch_kind = volume ? 2 : (all_fused ? 1 : 3);
     } else {
         ds->last_batch_kind = 0;
         Sink sink;

@@ -162,12 +162,47 @@ BATCH_GEOMETRIES = {
     # name: (geometry, frames in the batch, expected batch path)
     "2d": (halving_geometry(1024, 512, 5), 7, 1),
     "2d_odd": (halving_geometry(1000, 333, 4), 7, 1),
-    "2d_generic": (halving_geometry(1001, 333, 3), 5, 0),               # odd width
+    "2d_generic": (halving_geometry(1001, 333, 3), 5, 1),               # odd width
     "3d_odd_stack": ([(256, 128, 6), (128, 64, 3), (64, 32, 2)], 7, 0),  # per-frame
     "3d_fused": ([(256, 128, 8), (128, 64, 4), (64, 32, 2)], 8, 2),      # volume
     "3d_fused_deep": ([(512, 256, 16), (256, 128, 8), (128, 64, 4), (64, 32, 2)], 16, 2),
     "3d_fused_edge": ([(200, 61, 8), (100, 31, 4), (50, 16, 2)], 8, 2),  # odd rows
+    # narrow tiles (half the columns per lane): u8 512 wide (a wide wave
+    # would span 1024 px), 520 wide (only the narrow tile divides u8 rows)
+    "2d_narrow": (halving_geometry(512, 512, 3), 9, 1),
+    "2d_narrow_odd": (halving_geometry(520, 301, 3), 5, 1),
+    # six levels: a second fused run from a 63 x 38 level
+    "2d_six": (halving_geometry(1000, 600, 6), 3, 1),
 }
+
+
+def expected_2d_kind(geo, bpp):
+    """Restates cascade_pick_cols / the batch planner: a 2-D batch is kind 1
+    when every run of up to 4 XY levels fits the fused cascade with the wide
+    (16 B per lane, 32 B for 4/8-byte types) or the narrow (half) tile, and
+    kind 3 (the other runs on batched single-level kernels) otherwise."""
+    cw = (32 if bpp >= 4 else 16) // bpp
+    cn = cw // 2
+
+    def fits(L, k, c):
+        W, H, _ = geo[L - 1]
+        lb = min(16, c * bpp)
+        if W % c or (W * H * bpp) % lb:
+            return False
+        for i in range(k):
+            w, h, _ = geo[L + i]
+            sw = max((c * bpp) >> (i + 1), bpp)
+            if (w * h * bpp) % sw:
+                return False
+        return True
+
+    L = 1
+    while L < len(geo):
+        k = min(len(geo) - L, 4)
+        if not (fits(L, k, cw) or fits(L, k, cn)):
+            return 3
+        L += k
+    return 1
 
 
 @pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32, np.int64],
@@ -197,9 +232,11 @@ def test_device_batch_matches_stream(aqz, oracle, dtype, method, geo_kind):
                                  [0] + [o.data_ptr() for o in outs[1:]],
                                  launch_stream())
     torch.cuda.synchronize()
-    # the fused paths need 16-byte rows (W a multiple of 16 B of the dtype);
-    # other widths take the per-frame generic path
-    if (w * bpp) % 16 != 0:
+    # the fused 2-D cascade needs every run to fit a wide or narrow tile; the
+    # volume kernel needs 16-byte rows; anything else goes per-frame
+    if kind == 1:
+        kind = expected_2d_kind(geo, bpp)
+    elif kind == 2 and (w * bpp) % 16 != 0:
         kind = 0
     assert ds.last_batch_kind() == kind
     for L in expected:
@@ -319,7 +356,8 @@ def test_reference_example_stream(aqz, oracle):
         assert ds.take_frame(1) is None and ref.take_frame(1) is None
 
 
-@pytest.mark.parametrize("geo_kind", ["2d", "3d_odd_stack", "3d_fused", "2d_generic"])
+@pytest.mark.parametrize("geo_kind", ["2d", "3d_odd_stack", "3d_fused", "2d_generic",
+                                      "2d_six", "2d_narrow_odd"])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_host_batch_pipeline(aqz, oracle, geo_kind, pinned):
     """aqz_ds_run_host_batch: double-buffered groups over three streams must
