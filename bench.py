@@ -297,6 +297,12 @@ def main():
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
                 "min_launch_us": round(min(launch_ms) * 1e3, 2)}
 
+    ceiling = measure_ceiling(torch, stream, d_in, B * frame_bytes, alg_bytes - B * frame_bytes,
+                              max(5, args.steps // 2))
+    if ceiling is not None:
+        ceiling["frac_of_ceiling"] = round(achieved / ceiling["GBps"], 4)
+        roofline["same_mix_ceiling"] = ceiling
+
     cpu_baseline = None
     e2e = None
     if rank == 0 and world == 1 and not args.no_pmc:
@@ -430,6 +436,53 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
     orc_mod.transpose_frame(frame)
     res["transpose_kernel"]["cpu_reference_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
     return res
+
+
+def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
+    """Measured HBM ceiling for the kernel's own byte mix (tools/hbm_probe.hip):
+    a contiguous non-temporal stream reading the same input buffer and writing
+    in the nearest of the ratios 12:4, 13:3, 14:2 (4 KiB blocks per
+    workgroup), plus a read-only pass, timed with HIP events on the launch
+    stream.  A measurement aid, not product code: skipped (None) if the probe
+    library was not built."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libaqz_hbm_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.aqz_hbm_probe.restype = ctypes.c_int
+    lib.aqz_hbm_probe.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    frac_r = read_bytes / max(1, read_bytes + write_bytes)
+    rd, wr = min(((12, 4), (13, 3), (14, 2)), key=lambda m: abs(m[0] / 16 - frac_r))
+    dst = torch.empty(read_bytes // rd * wr + 4096, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, (r, w) in (("GBps", (rd, wr)), ("read_only_GBps", (16, 0))):
+        moved = ctypes.c_uint64(0)
+
+        def go():
+            rc = lib.aqz_hbm_probe(d_in.data_ptr(), read_bytes, dst.data_ptr(),
+                                   sink.data_ptr(), r, w, stream.cuda_stream,
+                                   ctypes.byref(moved))
+            if rc != 0:
+                raise RuntimeError(f"aqz_hbm_probe failed: {rc}")
+        for _ in range(3):
+            go()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            go()
+            b.record(stream)
+        torch.cuda.synchronize()
+        us = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e3
+        out[name] = round(moved.value / (us * 1e-6) / 1e9, 1)
+    out["read_write"] = f"{rd}:{wr}"
+    out["kernel"] = ("tools/hbm_probe.hip: contiguous nt loads/stores, one 4 KiB-block "
+                     "round per workgroup, same input buffer and stream")
+    return out
 
 
 def measure_traffic(args, kernel):

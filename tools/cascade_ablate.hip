@@ -94,7 +94,7 @@ cascade_ablate(CascadeParams p, uint32_t* sink)
     }
     uint32_t acc = 0;
     ablate_level<MASK, C, 1, NL, R, C>(p, v, f, row0, col0, lane, acc);
-    if (acc == 0xDEADBEEFu)
+    if (acc == 0xBEEFu) // u16 xors stay below 2^16
         sink[0] = acc;
 }
 
