@@ -315,6 +315,10 @@ def main():
             nf = min(B, 8)
             frames = d_in[:nf * frame_bytes].cpu().numpy().view(dtype).reshape(nf, H, W)
             cpu_baseline = measure_cpu(geo, dtype, method, args.cpu_seconds, list(frames))
+            threads = min(16, os.cpu_count() or 1)  # the box's CPU share is 16
+            if threads > 1:
+                cpu_baseline["parallel"] = measure_cpu_parallel(
+                    geo, dtype, method, max(2.0, args.cpu_seconds / 2), list(frames), threads)
         if args.e2e_frames > 0:
             e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device,
                               tile=(chunk, chunk))
@@ -564,6 +568,54 @@ def measure_cpu(geo, dtype, method, seconds, frames):
                       f"{n_levels}-level pyramid ({el:.1f} s): oracle/ds_oracle.c "
                       f"Downsampler add_frame+take_frame, single thread (-O3 -mavx2)",
             "ms_per_frame": round(el / n * 1e3, 3)}
+
+
+def measure_cpu_parallel(geo, dtype, method, seconds, frames, threads):
+    """Upper-bound CPU figure: `threads` host threads, each driving its own
+    oracle Downsampler over its own frames (independent streams, sharded
+    like the GPUs shard frames).  ctypes releases the GIL inside the C calls,
+    so the threads run the C oracle concurrently.  The reference itself runs
+    one downsampler per stream on one consumer thread
+    (zarr.stream.cpp:1616-1630); this is what a host with `threads` free
+    cores could do with as many streams."""
+    import threading
+    import oracle as orc_mod  # cpu_baseline leg only
+    W, H, _ = geo[0]
+    n_levels = len(geo)
+    counts = [0] * threads
+    start = threading.Barrier(threads + 1)
+    stop = threading.Event()
+
+    def worker(k):
+        ref = orc_mod.OracleDownsampler(geo, dtype, method)
+        for i in range(2):  # warm
+            ref.add_frame(frames[(k + i) % len(frames)])
+            for L in range(1, n_levels):
+                ref.take_frame(L)
+        start.wait()
+        n = 0
+        while not stop.is_set():
+            ref.add_frame(frames[(k + n) % len(frames)])
+            for L in range(1, n_levels):
+                ref.take_frame(L)
+            n += 1
+        counts[k] = n
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    start.wait()
+    t0 = time.perf_counter()
+    time.sleep(seconds)
+    stop.set()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    n = sum(counts)
+    return {"value": round(n * W * H / el / 1e9, 4), "unit": "GPixels/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} frames of {W}x{H} {np.dtype(dtype).name} over {threads} "
+                      f"threads, one oracle Downsampler each ({el:.1f} s)"}
 
 
 def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
