@@ -16,6 +16,7 @@
 // slot, so an untaken frame is never overwritten — the reference's
 // unordered_map::emplace rule.
 #include "aqz_downsampler.h"
+#include "abi_guard.hh"
 #include "ds_kernels.hh"
 
 #include <hip/hip_runtime.h>
@@ -174,6 +175,16 @@ struct aqz_ds
     // where a new level-L frame is written: never the cached slot
     void* out_slot(uint32_t L) const { return slot_ptr(L, cached[L] == 0 ? 1 : 0); }
 };
+
+namespace aqz {
+
+inline std::string*
+abi_err_slot(aqz_ds* ds)
+{
+    return ds ? &ds->err : nullptr;
+}
+
+} // namespace aqz
 
 namespace {
 
@@ -507,7 +518,12 @@ async_worker(aqz_ds* ds)
             return; // stop requested and nothing pending
         const void* frame = a.frame;
         lk.unlock();
-        const int rc = add_host_frame(ds, frame);
+        int rc;
+        try {
+            rc = add_host_frame(ds, frame);
+        } catch (...) {
+            rc = ABI_GUARD_FAIL(ds); // reported by the next settle()
+        }
         lk.lock();
         a.rc = rc;
         a.frame = nullptr;
@@ -597,49 +613,53 @@ aqz_plan_levels(const aqz_dimension* dims,
                 uint32_t out_cap_levels,
                 uint32_t* n_levels)
 {
-    if (!dims || !n_levels || ndims < 3 || ndims > AQZ_MAX_DIMS) {
-        set_global_error("plan_levels: need 3..%d dimensions", AQZ_MAX_DIMS);
-        return AQZ_INVALID_ARGUMENT;
-    }
-    for (uint32_t i = 0; i < ndims; ++i) {
-        if (dims[i].chunk_size_px == 0) {
-            set_global_error("plan_levels: dimension %u has chunk size 0", i);
+    try {
+        if (!dims || !n_levels || ndims < 3 || ndims > AQZ_MAX_DIMS) {
+            set_global_error("plan_levels: need 3..%d dimensions", AQZ_MAX_DIMS);
             return AQZ_INVALID_ARGUMENT;
         }
-    }
-    const aqz_dimension& x = dims[ndims - 1];
-    const aqz_dimension& y = dims[ndims - 2];
-    const aqz_dimension& z = dims[ndims - 3];
-    uint32_t levels = std::min(divisions(x), divisions(y));
-    if (z.type == AQZ_DIM_SPACE)
-        levels = std::max(levels, divisions(z));
-    if (max_levels > 0)
-        levels = std::min(levels, max_levels);
-    *n_levels = levels + 1;
-    if (!out)
+        for (uint32_t i = 0; i < ndims; ++i) {
+            if (dims[i].chunk_size_px == 0) {
+                set_global_error("plan_levels: dimension %u has chunk size 0", i);
+                return AQZ_INVALID_ARGUMENT;
+            }
+        }
+        const aqz_dimension& x = dims[ndims - 1];
+        const aqz_dimension& y = dims[ndims - 2];
+        const aqz_dimension& z = dims[ndims - 3];
+        uint32_t levels = std::min(divisions(x), divisions(y));
+        if (z.type == AQZ_DIM_SPACE)
+            levels = std::max(levels, divisions(z));
+        if (max_levels > 0)
+            levels = std::min(levels, max_levels);
+        *n_levels = levels + 1;
+        if (!out)
+            return AQZ_OK;
+        if (out_cap_levels < levels + 1) {
+            set_global_error("plan_levels: room for %u levels, need %u",
+                             out_cap_levels, levels + 1);
+            return AQZ_OVERFLOW;
+        }
+        std::copy(dims, dims + ndims, out);
+        for (uint32_t l = 1; l <= levels; ++l) {
+            const aqz_dimension* p = out + size_t(l - 1) * ndims;
+            aqz_dimension* c = out + size_t(l) * ndims;
+            std::copy(p, p + ndims - 3, c);
+            const aqz_dimension& pz = p[ndims - 3];
+            c[ndims - 3] = (pz.type == AQZ_DIM_SPACE && pz.array_size_px > pz.chunk_size_px)
+                             ? halve(pz)
+                             : pz;
+            const aqz_dimension& py = p[ndims - 2];
+            const aqz_dimension& px = p[ndims - 1];
+            const bool shrink_xy = std::min(py.array_size_px, px.array_size_px) >
+                                   std::max(py.chunk_size_px, px.chunk_size_px);
+            c[ndims - 2] = shrink_xy ? halve(py) : py;
+            c[ndims - 1] = shrink_xy ? halve(px) : px;
+        }
         return AQZ_OK;
-    if (out_cap_levels < levels + 1) {
-        set_global_error("plan_levels: room for %u levels, need %u",
-                         out_cap_levels, levels + 1);
-        return AQZ_OVERFLOW;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
     }
-    std::copy(dims, dims + ndims, out);
-    for (uint32_t l = 1; l <= levels; ++l) {
-        const aqz_dimension* p = out + size_t(l - 1) * ndims;
-        aqz_dimension* c = out + size_t(l) * ndims;
-        std::copy(p, p + ndims - 3, c);
-        const aqz_dimension& pz = p[ndims - 3];
-        c[ndims - 3] = (pz.type == AQZ_DIM_SPACE && pz.array_size_px > pz.chunk_size_px)
-                         ? halve(pz)
-                         : pz;
-        const aqz_dimension& py = p[ndims - 2];
-        const aqz_dimension& px = p[ndims - 1];
-        const bool shrink_xy = std::min(py.array_size_px, px.array_size_px) >
-                               std::max(py.chunk_size_px, px.chunk_size_px);
-        c[ndims - 2] = shrink_xy ? halve(py) : py;
-        c[ndims - 1] = shrink_xy ? halve(px) : px;
-    }
-    return AQZ_OK;
 }
 
 int
@@ -650,178 +670,202 @@ aqz_ds_create(const aqz_level_desc* levels,
               int device,
               aqz_ds** out)
 {
-    if (!out) {
-        set_global_error("create: null output handle");
-        return AQZ_INVALID_ARGUMENT;
-    }
-    *out = nullptr;
-    if (!levels || n_levels == 0 || n_levels > AQZ_MAX_LEVELS) {
-        set_global_error("create: need 1..%d levels", AQZ_MAX_LEVELS);
-        return AQZ_INVALID_ARGUMENT;
-    }
-    if (!aqz::dtype_valid(dtype)) {
-        set_global_error("Invalid data type: %d", dtype);
-        return AQZ_INVALID_ARGUMENT;
-    }
-    if (!aqz::method_valid(method)) {
-        set_global_error("Invalid downsampling method: %d", method);
-        return AQZ_INVALID_ARGUMENT;
-    }
-    for (uint32_t l = 0; l < n_levels; ++l) {
-        if (levels[l].width == 0 || levels[l].height == 0) {
-            set_global_error("create: level %u has an empty frame", l);
+    try {
+        if (!out) {
+            set_global_error("create: null output handle");
             return AQZ_INVALID_ARGUMENT;
         }
-        if (l > 0) {
-            const aqz_level_desc& a = levels[l - 1];
-            const aqz_level_desc& b = levels[l];
-            const bool same = b.width == a.width && b.height == a.height;
-            const bool half = b.width == (a.width + 1) / 2 &&
-                              b.height == (a.height + 1) / 2;
-            // scale_image always halves both; anything else fails the
-            // reference's dimension EXPECTs (downsampler.cpp:348-356).
-            if (!same && !half) {
-                set_global_error("create: level %u is neither a copy nor a 2x "
-                                 "reduction of level %u", l, l - 1);
+        *out = nullptr;
+        if (!levels || n_levels == 0 || n_levels > AQZ_MAX_LEVELS) {
+            set_global_error("create: need 1..%d levels", AQZ_MAX_LEVELS);
+            return AQZ_INVALID_ARGUMENT;
+        }
+        if (!aqz::dtype_valid(dtype)) {
+            set_global_error("Invalid data type: %d", dtype);
+            return AQZ_INVALID_ARGUMENT;
+        }
+        if (!aqz::method_valid(method)) {
+            set_global_error("Invalid downsampling method: %d", method);
+            return AQZ_INVALID_ARGUMENT;
+        }
+        for (uint32_t l = 0; l < n_levels; ++l) {
+            if (levels[l].width == 0 || levels[l].height == 0) {
+                set_global_error("create: level %u has an empty frame", l);
                 return AQZ_INVALID_ARGUMENT;
             }
+            if (l > 0) {
+                const aqz_level_desc& a = levels[l - 1];
+                const aqz_level_desc& b = levels[l];
+                const bool same = b.width == a.width && b.height == a.height;
+                const bool half = b.width == (a.width + 1) / 2 &&
+                                  b.height == (a.height + 1) / 2;
+                // scale_image always halves both; anything else fails the
+                // reference's dimension EXPECTs (downsampler.cpp:348-356).
+                if (!same && !half) {
+                    set_global_error("create: level %u is neither a copy nor a 2x "
+                                     "reduction of level %u", l, l - 1);
+                    return AQZ_INVALID_ARGUMENT;
+                }
+            }
         }
-    }
 
-    if (device < 0) {
-        const char* env = std::getenv("AQZ_GPU_DEVICE");
-        if (env && *env) {
-            device = std::atoi(env);
-        } else if (hipGetDevice(&device) != hipSuccess) {
-            device = 0;
+        if (device < 0) {
+            const char* env = std::getenv("AQZ_GPU_DEVICE");
+            if (env && *env) {
+                device = std::atoi(env);
+            } else if (hipGetDevice(&device) != hipSuccess) {
+                device = 0;
+            }
         }
-    }
 
-    auto* ds = new aqz_ds();
-    ds->device = device;
-    ds->dtype = dtype;
-    ds->method = method;
-    ds->bpp = aqz::dtype_bytes(dtype);
-    ds->n = n_levels;
-    ds->lv.assign(levels, levels + n_levels);
-    ds->bytes.resize(n_levels);
-    ds->xy.assign(n_levels, 0);
-    ds->zh.assign(n_levels, 0);
-    ds->count.assign(n_levels, 0);
-    ds->has_partial.assign(n_levels, 0);
-    ds->slot.assign(n_levels, { nullptr, nullptr });
-    ds->cached.assign(n_levels, -1);
-    ds->d_partial.assign(n_levels, nullptr);
-    ds->staged = env_flag("AQZ_PINNED_STAGING");
-    ds->tiling.assign(n_levels, { 0, 0 });
-    ds->tslot.assign(n_levels, { nullptr, nullptr });
-    ds->tflags.assign(n_levels, { nullptr, nullptr });
-    ds->tiled_for.assign(n_levels, -1);
-    for (uint32_t l = 0; l < n_levels; ++l) {
-        ds->bytes[l] = size_t(levels[l].width) * levels[l].height * ds->bpp;
-        if (l > 0) {
-            ds->xy[l] = levels[l].width < levels[l - 1].width ||
-                        levels[l].height < levels[l - 1].height;
-            ds->zh[l] = levels[l].planes < levels[l - 1].planes;
+        auto* ds = new aqz_ds();
+        ds->device = device;
+        ds->dtype = dtype;
+        ds->method = method;
+        ds->bpp = aqz::dtype_bytes(dtype);
+        ds->n = n_levels;
+        ds->lv.assign(levels, levels + n_levels);
+        ds->bytes.resize(n_levels);
+        ds->xy.assign(n_levels, 0);
+        ds->zh.assign(n_levels, 0);
+        ds->count.assign(n_levels, 0);
+        ds->has_partial.assign(n_levels, 0);
+        ds->slot.assign(n_levels, { nullptr, nullptr });
+        ds->cached.assign(n_levels, -1);
+        ds->d_partial.assign(n_levels, nullptr);
+        ds->staged = env_flag("AQZ_PINNED_STAGING");
+        ds->tiling.assign(n_levels, { 0, 0 });
+        ds->tslot.assign(n_levels, { nullptr, nullptr });
+        ds->tflags.assign(n_levels, { nullptr, nullptr });
+        ds->tiled_for.assign(n_levels, -1);
+        for (uint32_t l = 0; l < n_levels; ++l) {
+            ds->bytes[l] = size_t(levels[l].width) * levels[l].height * ds->bpp;
+            if (l > 0) {
+                ds->xy[l] = levels[l].width < levels[l - 1].width ||
+                            levels[l].height < levels[l - 1].height;
+                ds->zh[l] = levels[l].planes < levels[l - 1].planes;
+            }
         }
-    }
 
-    auto fail = [&](hipError_t e, const char* what) {
-        const int code = e == hipErrorOutOfMemory ? AQZ_OUT_OF_MEMORY
-                                                  : AQZ_INTERNAL_ERROR;
-        set_global_error("%s: %s", what, hipGetErrorString(e));
-        release(ds);
-        return code;
-    };
-    hipError_t e = hipSetDevice(device);
-    if (e != hipSuccess)
-        return fail(e, "hipSetDevice");
-    if ((e = hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking)) != hipSuccess)
-        return fail(e, "hipStreamCreate");
-    if ((e = hipEventCreateWithFlags(&ds->h2d_done, hipEventDisableTiming)) != hipSuccess)
-        return fail(e, "hipEventCreate");
-    if ((e = hipMalloc(&ds->d_in, ds->bytes[0])) != hipSuccess)
-        return fail(e, "hipMalloc level 0");
-    if (ds->staged &&
-        (e = hipHostMalloc(&ds->h_stage, ds->bytes[0], hipHostMallocDefault)) != hipSuccess)
-        return fail(e, "hipHostMalloc staging");
-    ds->device_bytes = ds->bytes[0];
-    for (uint32_t l = 1; l < n_levels; ++l) {
-        if ((e = hipMalloc(&ds->slot[l].first, ds->bytes[l])) != hipSuccess)
-            return fail(e, "hipMalloc level");
-        if ((e = hipMalloc(&ds->slot[l].second, ds->bytes[l])) != hipSuccess)
-            return fail(e, "hipMalloc level");
-        ds->device_bytes += 2 * ds->bytes[l];
-        if (ds->zh[l]) {
-            if ((e = hipMalloc(&ds->d_partial[l], ds->bytes[l])) != hipSuccess)
-                return fail(e, "hipMalloc partial");
-            ds->device_bytes += ds->bytes[l];
+        auto fail = [&](hipError_t e, const char* what) {
+            const int code = e == hipErrorOutOfMemory ? AQZ_OUT_OF_MEMORY
+                                                      : AQZ_INTERNAL_ERROR;
+            set_global_error("%s: %s", what, hipGetErrorString(e));
+            release(ds);
+            return code;
+        };
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess)
+            return fail(e, "hipSetDevice");
+        if ((e = hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking)) != hipSuccess)
+            return fail(e, "hipStreamCreate");
+        if ((e = hipEventCreateWithFlags(&ds->h2d_done, hipEventDisableTiming)) != hipSuccess)
+            return fail(e, "hipEventCreate");
+        if ((e = hipMalloc(&ds->d_in, ds->bytes[0])) != hipSuccess)
+            return fail(e, "hipMalloc level 0");
+        if (ds->staged &&
+            (e = hipHostMalloc(&ds->h_stage, ds->bytes[0], hipHostMallocDefault)) != hipSuccess)
+            return fail(e, "hipHostMalloc staging");
+        ds->device_bytes = ds->bytes[0];
+        for (uint32_t l = 1; l < n_levels; ++l) {
+            if ((e = hipMalloc(&ds->slot[l].first, ds->bytes[l])) != hipSuccess)
+                return fail(e, "hipMalloc level");
+            if ((e = hipMalloc(&ds->slot[l].second, ds->bytes[l])) != hipSuccess)
+                return fail(e, "hipMalloc level");
+            ds->device_bytes += 2 * ds->bytes[l];
+            if (ds->zh[l]) {
+                if ((e = hipMalloc(&ds->d_partial[l], ds->bytes[l])) != hipSuccess)
+                    return fail(e, "hipMalloc partial");
+                ds->device_bytes += ds->bytes[l];
+            }
         }
+        *out = ds;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
     }
-    *out = ds;
-    return AQZ_OK;
 }
 
 void
 aqz_ds_destroy(aqz_ds* ds)
 {
-    release(ds);
+    try {
+        release(ds);
+    } catch (...) {
+        (void)ABI_GUARD_FAIL(nullptr);
+    }
 }
 
 int
 aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame"))
-        return rc;
-    return add_host_frame(ds, host_frame);
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame"))
+            return rc;
+        return add_host_frame(ds, host_frame);
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
 }
 
 int
 aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame_async"))
-        return rc;
-    auto& a = ds->async;
-    if (!a.worker.joinable())
-        a.worker = std::thread(async_worker, ds);
-    {
-        std::lock_guard<std::mutex> lk(a.m);
-        a.frame = host_frame;
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame_async"))
+            return rc;
+        auto& a = ds->async;
+        if (!a.worker.joinable())
+            a.worker = std::thread(async_worker, ds);
+        {
+            std::lock_guard<std::mutex> lk(a.m);
+            a.frame = host_frame;
+        }
+        a.cv.notify_all();
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
     }
-    a.cv.notify_all();
-    return AQZ_OK;
 }
 
 int
 aqz_ds_wait(aqz_ds* ds)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    return settle(ds);
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        return settle(ds);
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
 }
 
 int
 aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (!device_frame || nbytes != ds->bytes[0])
-        return ds->fail_arg("add_device_frame: expected " +
-                            std::to_string(ds->bytes[0]) + " bytes, got " +
-                            std::to_string(nbytes));
-    if (int rc = bind_device(ds))
-        return rc;
-    return process_input(ds, device_frame);
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (!device_frame || nbytes != ds->bytes[0])
+            return ds->fail_arg("add_device_frame: expected " +
+                                std::to_string(ds->bytes[0]) + " bytes, got " +
+                                std::to_string(nbytes));
+        if (int rc = bind_device(ds))
+            return rc;
+        return process_input(ds, device_frame);
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
 }
 
 int
@@ -832,72 +876,80 @@ aqz_ds_take_frame(aqz_ds* ds,
                   size_t* nbytes,
                   int* has_frame)
 {
-    if (!ds || !has_frame)
-        return AQZ_INVALID_ARGUMENT;
-    *has_frame = 0;
-    if (int rc = settle(ds))
-        return rc;
-    if (level == 0 || level >= ds->n)
-        return AQZ_OK; // the reference's map lookup simply misses
-    if (ds->cached[level] < 0)
+    try {
+        if (!ds || !has_frame)
+            return AQZ_INVALID_ARGUMENT;
+        *has_frame = 0;
+        if (int rc = settle(ds))
+            return rc;
+        if (level == 0 || level >= ds->n)
+            return AQZ_OK; // the reference's map lookup simply misses
+        if (ds->cached[level] < 0)
+            return AQZ_OK;
+        *has_frame = 1;
+        if (nbytes)
+            *nbytes = ds->bytes[level];
+        if (!dst)
+            return AQZ_OK;
+        if (cap < ds->bytes[level])
+            return ds->fail_arg("take_frame: buffer too small");
+        if (int rc = bind_device(ds))
+            return rc;
+        // HBM -> caller memory directly (stream-ordered after the kernels)
+        HIP_TRY(ds,
+                hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
+                               ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
+                "hipMemcpyAsync D2H");
+        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        ds->cached[level] = -1;
+        ds->tiled_for[level] = -1;
         return AQZ_OK;
-    *has_frame = 1;
-    if (nbytes)
-        *nbytes = ds->bytes[level];
-    if (!dst)
-        return AQZ_OK;
-    if (cap < ds->bytes[level])
-        return ds->fail_arg("take_frame: buffer too small");
-    if (int rc = bind_device(ds))
-        return rc;
-    // HBM -> caller memory directly (stream-ordered after the kernels)
-    HIP_TRY(ds,
-            hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
-                           ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
-            "hipMemcpyAsync D2H");
-    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-    ds->cached[level] = -1;
-    ds->tiled_for[level] = -1;
-    return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
 }
 
 int
 aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t tile_cols)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (level == 0 || level >= ds->n)
-        return ds->fail_arg("set_level_tiling: bad level " + std::to_string(level));
-    if ((tile_rows == 0) != (tile_cols == 0))
-        return ds->fail_arg("set_level_tiling: tile rows/cols must both be 0 or >0");
-    if (int rc = bind_device(ds))
-        return rc;
-    HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-    auto& t = ds->tslot[level];
-    (void)hipFree(t.first);
-    (void)hipFree(t.second);
-    t = { nullptr, nullptr };
-    auto& tf = ds->tflags[level];
-    (void)hipHostFree(tf.first);
-    (void)hipHostFree(tf.second);
-    tf = { nullptr, nullptr };
-    ds->tiling[level] = { 0, 0 };
-    ds->tiled_for[level] = -1;
-    if (tile_rows == 0)
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (level == 0 || level >= ds->n)
+            return ds->fail_arg("set_level_tiling: bad level " + std::to_string(level));
+        if ((tile_rows == 0) != (tile_cols == 0))
+            return ds->fail_arg("set_level_tiling: tile rows/cols must both be 0 or >0");
+        if (int rc = bind_device(ds))
+            return rc;
+        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        auto& t = ds->tslot[level];
+        (void)hipFree(t.first);
+        (void)hipFree(t.second);
+        t = { nullptr, nullptr };
+        auto& tf = ds->tflags[level];
+        (void)hipHostFree(tf.first);
+        (void)hipHostFree(tf.second);
+        tf = { nullptr, nullptr };
+        ds->tiling[level] = { 0, 0 };
+        ds->tiled_for[level] = -1;
+        if (tile_rows == 0)
+            return AQZ_OK;
+        const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
+        HIP_TRY(ds, hipMalloc(&t.first, g.tile_bytes), "hipMalloc tiles");
+        HIP_TRY(ds, hipMalloc(&t.second, g.tile_bytes), "hipMalloc tiles");
+        // slice flags live in pinned host memory the kernel writes directly, so
+        // take_frame_tiled needs no separate flag copy
+        HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.first), g.flag_bytes,
+                                  hipHostMallocDefault), "hipHostMalloc flags");
+        HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.second), g.flag_bytes,
+                                  hipHostMallocDefault), "hipHostMalloc flags");
+        ds->tiling[level] = { tile_rows, tile_cols };
         return AQZ_OK;
-    const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
-    HIP_TRY(ds, hipMalloc(&t.first, g.tile_bytes), "hipMalloc tiles");
-    HIP_TRY(ds, hipMalloc(&t.second, g.tile_bytes), "hipMalloc tiles");
-    // slice flags live in pinned host memory the kernel writes directly, so
-    // take_frame_tiled needs no separate flag copy
-    HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.first), g.flag_bytes,
-                              hipHostMallocDefault), "hipHostMalloc flags");
-    HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.second), g.flag_bytes,
-                              hipHostMallocDefault), "hipHostMalloc flags");
-    ds->tiling[level] = { tile_rows, tile_cols };
-    return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
 }
 
 int
@@ -911,60 +963,68 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
                         size_t* nbytes,
                         int* has_frame)
 {
-    if (!ds || !has_frame)
-        return AQZ_INVALID_ARGUMENT;
-    *has_frame = 0;
-    if (int rc = settle(ds))
-        return rc;
-    if (tile_rows == 0 || tile_cols == 0)
-        return ds->fail_arg("take_frame_tiled: empty tile");
-    if (level == 0 || level >= ds->n || ds->cached[level] < 0)
-        return AQZ_OK;
-    const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
-    *has_frame = 1;
-    if (nbytes)
-        *nbytes = g.tile_bytes;
-    if (!dst)
-        return AQZ_OK;
-    if (cap < g.tile_bytes)
-        return ds->fail_arg("take_frame_tiled: buffer too small");
-    if (int rc = bind_device(ds))
-        return rc;
-    const int k = ds->cached[level];
-    if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
-        ds->tiled_for[level] == k) {
-        // tiled when the frame was emitted (aqz_ds_set_level_tiling)
-        if (int rc = tiles_to_host(ds, g,
-                                   k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
-                                   k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
-                                   dst, tile_nonzero))
+    try {
+        if (!ds || !has_frame)
+            return AQZ_INVALID_ARGUMENT;
+        *has_frame = 0;
+        if (int rc = settle(ds))
             return rc;
-    } else if (int rc = tile_to_host(ds, ds->slot_ptr(level, k), ds->lv[level], tile_rows,
-                                     tile_cols, g, dst, tile_nonzero)) {
-        return rc;
+        if (tile_rows == 0 || tile_cols == 0)
+            return ds->fail_arg("take_frame_tiled: empty tile");
+        if (level == 0 || level >= ds->n || ds->cached[level] < 0)
+            return AQZ_OK;
+        const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
+        *has_frame = 1;
+        if (nbytes)
+            *nbytes = g.tile_bytes;
+        if (!dst)
+            return AQZ_OK;
+        if (cap < g.tile_bytes)
+            return ds->fail_arg("take_frame_tiled: buffer too small");
+        if (int rc = bind_device(ds))
+            return rc;
+        const int k = ds->cached[level];
+        if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
+            ds->tiled_for[level] == k) {
+            // tiled when the frame was emitted (aqz_ds_set_level_tiling)
+            if (int rc = tiles_to_host(ds, g,
+                                       k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
+                                       k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
+                                       dst, tile_nonzero))
+                return rc;
+        } else if (int rc = tile_to_host(ds, ds->slot_ptr(level, k), ds->lv[level], tile_rows,
+                                         tile_cols, g, dst, tile_nonzero)) {
+            return rc;
+        }
+        ds->cached[level] = -1;
+        ds->tiled_for[level] = -1;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
     }
-    ds->cached[level] = -1;
-    ds->tiled_for[level] = -1;
-    return AQZ_OK;
 }
 
 int
 aqz_ds_set_input_transpose(aqz_ds* ds, int transpose)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (int rc = bind_device(ds))
-        return rc;
-    if (transpose && !ds->d_tin) {
-        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-        HIP_TRY(ds, hipMalloc(&ds->d_tin, ds->bytes[0]), "hipMalloc transposed input");
-        ds->device_bytes += ds->bytes[0];
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (int rc = bind_device(ds))
+            return rc;
+        if (transpose && !ds->d_tin) {
+            HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+            HIP_TRY(ds, hipMalloc(&ds->d_tin, ds->bytes[0]), "hipMalloc transposed input");
+            ds->device_bytes += ds->bytes[0];
+        }
+        ds->transpose = transpose != 0;
+        ds->last_input = nullptr;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
     }
-    ds->transpose = transpose != 0;
-    ds->last_input = nullptr;
-    return AQZ_OK;
 }
 
 int
@@ -977,41 +1037,45 @@ aqz_ds_take_input_frame(aqz_ds* ds,
                         size_t* nbytes,
                         int* has_frame)
 {
-    if (!ds || !has_frame)
-        return AQZ_INVALID_ARGUMENT;
-    *has_frame = 0;
-    if (int rc = settle(ds))
-        return rc;
-    if ((tile_rows == 0) != (tile_cols == 0))
-        return ds->fail_arg("take_input_frame: tile_rows and tile_cols must both be 0 "
-                            "or both be nonzero");
-    if (!ds->last_input)
-        return AQZ_OK;
-    const bool tiled = tile_rows != 0;
-    const TileGeom g = tiled ? tile_geom(ds, 0, tile_rows, tile_cols)
-                             : TileGeom{ 1, ds->bytes[0], 0 };
-    *has_frame = 1;
-    if (nbytes)
-        *nbytes = g.tile_bytes;
-    if (!dst)
-        return AQZ_OK;
-    if (cap < g.tile_bytes)
-        return ds->fail_arg("take_input_frame: buffer too small");
-    if (int rc = bind_device(ds))
-        return rc;
-    if (tiled) {
-        if (int rc = tile_to_host(ds, ds->last_input, ds->lv[0], tile_rows, tile_cols, g,
-                                  dst, tile_nonzero))
+    try {
+        if (!ds || !has_frame)
+            return AQZ_INVALID_ARGUMENT;
+        *has_frame = 0;
+        if (int rc = settle(ds))
             return rc;
-    } else {
-        HIP_TRY(ds,
-                hipMemcpyAsync(dst, ds->last_input, g.tile_bytes, hipMemcpyDeviceToHost,
-                               ds->stream),
-                "hipMemcpyAsync D2H");
-        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        if ((tile_rows == 0) != (tile_cols == 0))
+            return ds->fail_arg("take_input_frame: tile_rows and tile_cols must both be 0 "
+                                "or both be nonzero");
+        if (!ds->last_input)
+            return AQZ_OK;
+        const bool tiled = tile_rows != 0;
+        const TileGeom g = tiled ? tile_geom(ds, 0, tile_rows, tile_cols)
+                                 : TileGeom{ 1, ds->bytes[0], 0 };
+        *has_frame = 1;
+        if (nbytes)
+            *nbytes = g.tile_bytes;
+        if (!dst)
+            return AQZ_OK;
+        if (cap < g.tile_bytes)
+            return ds->fail_arg("take_input_frame: buffer too small");
+        if (int rc = bind_device(ds))
+            return rc;
+        if (tiled) {
+            if (int rc = tile_to_host(ds, ds->last_input, ds->lv[0], tile_rows, tile_cols, g,
+                                      dst, tile_nonzero))
+                return rc;
+        } else {
+            HIP_TRY(ds,
+                    hipMemcpyAsync(dst, ds->last_input, g.tile_bytes, hipMemcpyDeviceToHost,
+                                   ds->stream),
+                    "hipMemcpyAsync D2H");
+            HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        }
+        ds->last_input = nullptr;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
     }
-    ds->last_input = nullptr;
-    return AQZ_OK;
 }
 
 int
@@ -1022,17 +1086,21 @@ aqz_transpose_frame_device(int dtype,
                            void* device_dst,
                            void* hip_stream)
 {
-    if (!aqz::dtype_valid(dtype) || !device_src || !device_dst || rows == 0 || cols == 0) {
-        set_global_error("transpose_frame_device: invalid argument");
-        return AQZ_INVALID_ARGUMENT;
+    try {
+        if (!aqz::dtype_valid(dtype) || !device_src || !device_dst || rows == 0 || cols == 0) {
+            set_global_error("transpose_frame_device: invalid argument");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        const hipError_t e = aqz::launch_transpose(dtype, device_src, rows, cols, device_dst,
+                                                   static_cast<hipStream_t>(hip_stream));
+        if (e != hipSuccess) {
+            set_global_error("transpose_frame_device: %s", hipGetErrorString(e));
+            return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
+        }
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
     }
-    const hipError_t e = aqz::launch_transpose(dtype, device_src, rows, cols, device_dst,
-                                               static_cast<hipStream_t>(hip_stream));
-    if (e != hipSuccess) {
-        set_global_error("transpose_frame_device: %s", hipGetErrorString(e));
-        return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
-    }
-    return AQZ_OK;
 }
 
 int
@@ -1046,19 +1114,23 @@ aqz_tile_frame_device(int dtype,
                       uint32_t* device_nonzero,
                       void* hip_stream)
 {
-    if (!aqz::dtype_valid(dtype) || !device_frame || !device_tiles ||
-        !device_nonzero) {
-        set_global_error("tile_frame_device: invalid argument");
-        return AQZ_INVALID_ARGUMENT;
+    try {
+        if (!aqz::dtype_valid(dtype) || !device_frame || !device_tiles ||
+            !device_nonzero) {
+            set_global_error("tile_frame_device: invalid argument");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        const hipError_t e = aqz::launch_tile_frame(
+          dtype, device_frame, width, height, tile_rows, tile_cols, device_tiles,
+          device_nonzero, static_cast<hipStream_t>(hip_stream));
+        if (e != hipSuccess) {
+            set_global_error("tile_frame_device: %s", hipGetErrorString(e));
+            return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
+        }
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
     }
-    const hipError_t e = aqz::launch_tile_frame(
-      dtype, device_frame, width, height, tile_rows, tile_cols, device_tiles,
-      device_nonzero, static_cast<hipStream_t>(hip_stream));
-    if (e != hipSuccess) {
-        set_global_error("tile_frame_device: %s", hipGetErrorString(e));
-        return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
-    }
-    return AQZ_OK;
 }
 
 uint32_t
@@ -1078,18 +1150,22 @@ aqz_tile_frame_device_sliced(int dtype,
                              uint8_t* device_slice_flags,
                              void* hip_stream)
 {
-    if (!aqz::dtype_valid(dtype) || !device_frame || !device_tiles || !device_slice_flags) {
-        set_global_error("tile_frame_device_sliced: invalid argument");
-        return AQZ_INVALID_ARGUMENT;
+    try {
+        if (!aqz::dtype_valid(dtype) || !device_frame || !device_tiles || !device_slice_flags) {
+            set_global_error("tile_frame_device_sliced: invalid argument");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        const hipError_t e = aqz::launch_tile_frame_sliced(
+          dtype, device_frame, width, height, tile_rows, tile_cols, device_tiles,
+          device_slice_flags, static_cast<hipStream_t>(hip_stream));
+        if (e != hipSuccess) {
+            set_global_error("tile_frame_device_sliced: %s", hipGetErrorString(e));
+            return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
+        }
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
     }
-    const hipError_t e = aqz::launch_tile_frame_sliced(
-      dtype, device_frame, width, height, tile_rows, tile_cols, device_tiles,
-      device_slice_flags, static_cast<hipStream_t>(hip_stream));
-    if (e != hipSuccess) {
-        set_global_error("tile_frame_device_sliced: %s", hipGetErrorString(e));
-        return e == hipErrorInvalidValue ? AQZ_INVALID_ARGUMENT : AQZ_INTERNAL_ERROR;
-    }
-    return AQZ_OK;
 }
 
 int
@@ -1100,140 +1176,144 @@ aqz_ds_run_device_batch(aqz_ds* ds,
                         uint32_t* out_counts,
                         void* hip_stream)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (ds->transpose)
-        return ds->fail_arg("ds_run_device_batch: input transposition applies to the per-frame path "
-                            "(add_frame / add_device_frame) only");
-    ds->last_input = nullptr;
-    if (!device_frames || !device_out_levels)
-        return ds->fail_arg("run_device_batch: null buffer");
-    for (uint32_t l = 1; l < ds->n; ++l)
-        if (!device_out_levels[l])
-            return ds->fail_arg("run_device_batch: null output for level " +
-                                std::to_string(l));
-    if (int rc = bind_device(ds))
-        return rc;
-    hipStream_t user = static_cast<hipStream_t>(hip_stream);
-    hipStream_t saved = ds->stream;
-    if (user)
-        ds->stream = user;
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (ds->transpose)
+            return ds->fail_arg("ds_run_device_batch: input transposition applies to the per-frame path "
+                                "(add_frame / add_device_frame) only");
+        ds->last_input = nullptr;
+        if (!device_frames || !device_out_levels)
+            return ds->fail_arg("run_device_batch: null buffer");
+        for (uint32_t l = 1; l < ds->n; ++l)
+            if (!device_out_levels[l])
+                return ds->fail_arg("run_device_batch: null output for level " +
+                                    std::to_string(l));
+        if (int rc = bind_device(ds))
+            return rc;
+        hipStream_t user = static_cast<hipStream_t>(hip_stream);
+        hipStream_t saved = ds->stream;
+        if (user)
+            ds->stream = user;
 
-    std::vector<uint32_t> emitted(ds->n, 0);
-    int rc = AQZ_OK;
+        std::vector<uint32_t> emitted(ds->n, 0);
+        int rc = AQZ_OK;
 
-    bool pure_xy = ds->n > 1;
-    bool pure_xyz = ds->n > 1;
-    for (uint32_t l = 1; l < ds->n; ++l) {
-        pure_xy = pure_xy && ds->xy[l] && !ds->zh[l];
-        // every level halves XY and Z, no odd stack (no pass-through plane)
-        // and no stored earlier plane: planes pair up consecutively
-        pure_xyz = pure_xyz && ds->xy[l] && ds->zh[l] &&
-                   ds->lv[l - 1].planes % 2 == 0 && !ds->has_partial[l];
-    }
-    pure_xyz = pure_xyz && n_frames > 0 && (n_frames % (1u << (ds->n - 1))) == 0;
+        bool pure_xy = ds->n > 1;
+        bool pure_xyz = ds->n > 1;
+        for (uint32_t l = 1; l < ds->n; ++l) {
+            pure_xy = pure_xy && ds->xy[l] && !ds->zh[l];
+            // every level halves XY and Z, no odd stack (no pass-through plane)
+            // and no stored earlier plane: planes pair up consecutively
+            pure_xyz = pure_xyz && ds->xy[l] && ds->zh[l] &&
+                       ds->lv[l - 1].planes % 2 == 0 && !ds->has_partial[l];
+        }
+        pure_xyz = pure_xyz && n_frames > 0 && (n_frames % (1u << (ds->n - 1))) == 0;
 
-    // Plan runs of up to `maxk` levels per launch.  A 2-D batch always stays
-    // batched: a run the fused cascade cannot take (width or alignment) runs
-    // as one batched single-level generic launch per level.  A volume batch
-    // is all-or-nothing (its fallback is the per-frame state machine).
-    struct Run
-    {
-        uint32_t L, k;
-        bool fused;
-    };
-    auto plan_runs = [&](uint32_t maxk, bool volume) {
+        // Plan runs of up to `maxk` levels per launch.  A 2-D batch always stays
+        // batched: a run the fused cascade cannot take (width or alignment) runs
+        // as one batched single-level generic launch per level.  A volume batch
+        // is all-or-nothing (its fallback is the per-frame state machine).
+        struct Run
+        {
+            uint32_t L, k;
+            bool fused;
+        };
+        auto plan_runs = [&](uint32_t maxk, bool volume) {
+            std::vector<Run> runs;
+            const void* src = device_frames;
+            for (uint32_t L = 1; L < ds->n;) {
+                const uint32_t k = std::min<uint32_t>(ds->n - L, maxk);
+                aqz::LevelOut o[aqz::kMaxFusedLevels];
+                for (uint32_t j = 0; j < k; ++j)
+                    o[j] = { device_out_levels[L + j], elems(ds, L + j),
+                             ds->lv[L + j].width, ds->lv[L + j].height };
+                const aqz_level_desc& a = ds->lv[L - 1];
+                const bool ok =
+                  volume ? aqz::volume_supported(ds->dtype, src, a.width, a.height, o, int(k))
+                         : aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width,
+                                                  a.height, o, int(k));
+                if (!ok && volume)
+                    return std::vector<Run>{};
+                runs.push_back({ L, k, ok });
+                src = o[k - 1].ptr;
+                L += k;
+            }
+            return runs;
+        };
+
         std::vector<Run> runs;
-        const void* src = device_frames;
-        for (uint32_t L = 1; L < ds->n;) {
-            const uint32_t k = std::min<uint32_t>(ds->n - L, maxk);
-            aqz::LevelOut o[aqz::kMaxFusedLevels];
-            for (uint32_t j = 0; j < k; ++j)
-                o[j] = { device_out_levels[L + j], elems(ds, L + j),
-                         ds->lv[L + j].width, ds->lv[L + j].height };
-            const aqz_level_desc& a = ds->lv[L - 1];
-            const bool ok =
-              volume ? aqz::volume_supported(ds->dtype, src, a.width, a.height, o, int(k))
-                     : aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width,
-                                              a.height, o, int(k));
-            if (!ok && volume)
-                return std::vector<Run>{};
-            runs.push_back({ L, k, ok });
-            src = o[k - 1].ptr;
-            L += k;
+        bool volume = false;
+        if (pure_xy && n_frames > 0) {
+            runs = plan_runs(aqz::kMaxFusedLevels, false);
+        } else if (pure_xyz) {
+            runs = plan_runs(aqz::kMaxVolumeLevels, true);
+            volume = true;
         }
-        return runs;
-    };
 
-    std::vector<Run> runs;
-    bool volume = false;
-    if (pure_xy && n_frames > 0) {
-        runs = plan_runs(aqz::kMaxFusedLevels, false);
-    } else if (pure_xyz) {
-        runs = plan_runs(aqz::kMaxVolumeLevels, true);
-        volume = true;
-    }
-
-    if (!runs.empty()) {
-        // Whole batch in batched launches; every frame / plane group independent.
-        const void* src = device_frames;
-        uint32_t planes = n_frames;
-        bool all_fused = true;
-        for (const Run& run : runs) {
-            aqz::LevelOut o[aqz::kMaxFusedLevels];
-            for (uint32_t j = 0; j < run.k; ++j)
-                o[j] = { device_out_levels[run.L + j], elems(ds, run.L + j),
-                         ds->lv[run.L + j].width, ds->lv[run.L + j].height };
-            const aqz_level_desc& a = ds->lv[run.L - 1];
-            hipError_t e = hipSuccess;
-            if (volume) {
-                e = aqz::launch_volume(ds->dtype, ds->method, src, elems(ds, run.L - 1),
-                                       a.width, a.height, o, int(run.k), planes, ds->stream);
-            } else if (run.fused) {
-                e = aqz::launch_cascade(ds->dtype, ds->method, src, elems(ds, run.L - 1),
-                                        a.width, a.height, o, int(run.k), n_frames,
-                                        ds->stream);
-            } else {
-                all_fused = false;
-                const void* s = src;
-                for (uint32_t j = 0; j < run.k && e == hipSuccess; ++j) {
-                    const aqz_level_desc& in = ds->lv[run.L + j - 1];
-                    e = aqz::launch_xy_generic(ds->dtype, ds->method, s,
-                                               elems(ds, run.L + j - 1), in.width, in.height,
-                                               o[j], n_frames, ds->stream);
-                    s = o[j].ptr;
+        if (!runs.empty()) {
+            // Whole batch in batched launches; every frame / plane group independent.
+            const void* src = device_frames;
+            uint32_t planes = n_frames;
+            bool all_fused = true;
+            for (const Run& run : runs) {
+                aqz::LevelOut o[aqz::kMaxFusedLevels];
+                for (uint32_t j = 0; j < run.k; ++j)
+                    o[j] = { device_out_levels[run.L + j], elems(ds, run.L + j),
+                             ds->lv[run.L + j].width, ds->lv[run.L + j].height };
+                const aqz_level_desc& a = ds->lv[run.L - 1];
+                hipError_t e = hipSuccess;
+                if (volume) {
+                    e = aqz::launch_volume(ds->dtype, ds->method, src, elems(ds, run.L - 1),
+                                           a.width, a.height, o, int(run.k), planes, ds->stream);
+                } else if (run.fused) {
+                    e = aqz::launch_cascade(ds->dtype, ds->method, src, elems(ds, run.L - 1),
+                                            a.width, a.height, o, int(run.k), n_frames,
+                                            ds->stream);
+                } else {
+                    all_fused = false;
+                    const void* s = src;
+                    for (uint32_t j = 0; j < run.k && e == hipSuccess; ++j) {
+                        const aqz_level_desc& in = ds->lv[run.L + j - 1];
+                        e = aqz::launch_xy_generic(ds->dtype, ds->method, s,
+                                                   elems(ds, run.L + j - 1), in.width, in.height,
+                                                   o[j], n_frames, ds->stream);
+                        s = o[j].ptr;
+                    }
                 }
+                if (e != hipSuccess) {
+                    rc = ds->fail(e, volume ? "batch volume" : "batch cascade");
+                    break;
+                }
+                src = o[run.k - 1].ptr;
+                if (volume)
+                    planes >>= run.k;
             }
-            if (e != hipSuccess) {
-                rc = ds->fail(e, volume ? "batch volume" : "batch cascade");
-                break;
+            for (uint32_t l = 0; l < ds->n; ++l) {
+                emitted[l] = volume ? (n_frames >> l) : n_frames;
+                ds->count[l] += emitted[l];
             }
-            src = o[run.k - 1].ptr;
-            if (volume)
-                planes >>= run.k;
+            ds->last_batch_kind = volume ? 2 : (all_fused ? 1 : 3);
+        } else {
+            ds->last_batch_kind = 0;
+            Sink sink;
+            sink.batch = true;
+            sink.out = device_out_levels;
+            sink.emitted = &emitted;
+            const uint8_t* base = static_cast<const uint8_t*>(device_frames);
+            for (uint32_t i = 0; i < n_frames && rc == AQZ_OK; ++i)
+                rc = process_frame(ds, base + size_t(i) * ds->bytes[0], sink);
+            emitted[0] = n_frames;
         }
-        for (uint32_t l = 0; l < ds->n; ++l) {
-            emitted[l] = volume ? (n_frames >> l) : n_frames;
-            ds->count[l] += emitted[l];
-        }
-        ds->last_batch_kind = volume ? 2 : (all_fused ? 1 : 3);
-    } else {
-        ds->last_batch_kind = 0;
-        Sink sink;
-        sink.batch = true;
-        sink.out = device_out_levels;
-        sink.emitted = &emitted;
-        const uint8_t* base = static_cast<const uint8_t*>(device_frames);
-        for (uint32_t i = 0; i < n_frames && rc == AQZ_OK; ++i)
-            rc = process_frame(ds, base + size_t(i) * ds->bytes[0], sink);
-        emitted[0] = n_frames;
+        if (out_counts)
+            std::copy(emitted.begin(), emitted.end(), out_counts);
+        ds->stream = saved;
+        return rc;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
     }
-    if (out_counts)
-        std::copy(emitted.begin(), emitted.end(), out_counts);
-    ds->stream = saved;
-    return rc;
 }
 
 namespace {
@@ -1298,85 +1378,89 @@ aqz_ds_run_host_batch(aqz_ds* ds,
                       void* const* host_out_levels,
                       uint32_t* out_counts)
 {
-    if (!ds)
-        return AQZ_INVALID_ARGUMENT;
-    if (int rc = settle(ds))
-        return rc;
-    if (ds->transpose)
-        return ds->fail_arg("ds_run_host_batch: input transposition applies to the per-frame path "
-                            "(add_frame / add_device_frame) only");
-    ds->last_input = nullptr;
-    if (!host_frames || !host_out_levels)
-        return ds->fail_arg("run_host_batch: null buffer");
-    for (uint32_t l = 1; l < ds->n; ++l)
-        if (!host_out_levels[l])
-            return ds->fail_arg("run_host_batch: null output for level " +
-                                std::to_string(l));
-    if (int rc = bind_device(ds))
-        return rc;
-    const uint32_t group = pipe_group(ds, n_frames);
-    if (int rc = ensure_pipe(ds, group))
-        return rc;
-    auto& p = ds->pipe;
-    std::vector<uint32_t> total(ds->n, 0);
-    const uint8_t* src = static_cast<const uint8_t*>(host_frames);
-    int rc = AQZ_OK;
-    uint32_t k = 0;
-    // Any failure below still drains all three streams before returning, so
-    // no copy is left reading or writing the caller's buffers.
-    auto drain = [&](int code) {
-        (void)hipStreamSynchronize(p.s_in);
-        (void)hipStreamSynchronize(p.s_work);
-        (void)hipStreamSynchronize(p.s_out);
-        return code;
-    };
-#define HIP_TRY_DRAIN(ds, expr, what)                                          \
-    do {                                                                       \
-        hipError_t e_ = (expr);                                                \
-        if (e_ != hipSuccess)                                                  \
-            return drain((ds)->fail(e_, what));                                \
-    } while (0)
-    for (uint32_t f0 = 0; f0 < n_frames && rc == AQZ_OK; f0 += group, ++k) {
-        const int b = int(k & 1);
-        const uint32_t g = std::min(group, n_frames - f0);
-        // upload: buffer b is free once group k-2's kernels are done with it
-        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_in, p.work_done[b], 0), "wait");
-        HIP_TRY_DRAIN(ds,
-                hipMemcpyAsync(p.d_in[b], src + size_t(f0) * ds->bytes[0],
-                               size_t(g) * ds->bytes[0], hipMemcpyHostToDevice,
-                               p.s_in),
-                "hipMemcpyAsync H2D");
-        HIP_TRY_DRAIN(ds, hipEventRecord(p.in_done[b], p.s_in), "event");
-        // kernels: after the upload, and after group k-2's download of d_out[b]
-        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_work, p.in_done[b], 0), "wait");
-        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_work, p.out_done[b], 0), "wait");
-        std::vector<uint32_t> counts(ds->n, 0);
-        rc = aqz_ds_run_device_batch(ds, p.d_in[b], g, p.d_out[b].data(),
-                                     counts.data(), p.s_work);
-        if (rc)
-            return drain(rc);
-        HIP_TRY_DRAIN(ds, hipEventRecord(p.work_done[b], p.s_work), "event");
-        // download every frame this group emitted, appended per level
-        HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_out, p.work_done[b], 0), "wait");
-        for (uint32_t l = 1; l < ds->n; ++l) {
-            if (!counts[l])
-                continue;
-            uint8_t* dst = static_cast<uint8_t*>(host_out_levels[l]) +
-                           size_t(total[l]) * ds->bytes[l];
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (ds->transpose)
+            return ds->fail_arg("ds_run_host_batch: input transposition applies to the per-frame path "
+                                "(add_frame / add_device_frame) only");
+        ds->last_input = nullptr;
+        if (!host_frames || !host_out_levels)
+            return ds->fail_arg("run_host_batch: null buffer");
+        for (uint32_t l = 1; l < ds->n; ++l)
+            if (!host_out_levels[l])
+                return ds->fail_arg("run_host_batch: null output for level " +
+                                    std::to_string(l));
+        if (int rc = bind_device(ds))
+            return rc;
+        const uint32_t group = pipe_group(ds, n_frames);
+        if (int rc = ensure_pipe(ds, group))
+            return rc;
+        auto& p = ds->pipe;
+        std::vector<uint32_t> total(ds->n, 0);
+        const uint8_t* src = static_cast<const uint8_t*>(host_frames);
+        int rc = AQZ_OK;
+        uint32_t k = 0;
+        // Any failure below still drains all three streams before returning, so
+        // no copy is left reading or writing the caller's buffers.
+        auto drain = [&](int code) {
+            (void)hipStreamSynchronize(p.s_in);
+            (void)hipStreamSynchronize(p.s_work);
+            (void)hipStreamSynchronize(p.s_out);
+            return code;
+        };
+    #define HIP_TRY_DRAIN(ds, expr, what)                                          \
+        do {                                                                       \
+            hipError_t e_ = (expr);                                                \
+            if (e_ != hipSuccess)                                                  \
+                return drain((ds)->fail(e_, what));                                \
+        } while (0)
+        for (uint32_t f0 = 0; f0 < n_frames && rc == AQZ_OK; f0 += group, ++k) {
+            const int b = int(k & 1);
+            const uint32_t g = std::min(group, n_frames - f0);
+            // upload: buffer b is free once group k-2's kernels are done with it
+            HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_in, p.work_done[b], 0), "wait");
             HIP_TRY_DRAIN(ds,
-                    hipMemcpyAsync(dst, p.d_out[b][l], size_t(counts[l]) * ds->bytes[l],
-                                   hipMemcpyDeviceToHost, p.s_out),
-                    "hipMemcpyAsync D2H");
-            total[l] += counts[l];
+                    hipMemcpyAsync(p.d_in[b], src + size_t(f0) * ds->bytes[0],
+                                   size_t(g) * ds->bytes[0], hipMemcpyHostToDevice,
+                                   p.s_in),
+                    "hipMemcpyAsync H2D");
+            HIP_TRY_DRAIN(ds, hipEventRecord(p.in_done[b], p.s_in), "event");
+            // kernels: after the upload, and after group k-2's download of d_out[b]
+            HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_work, p.in_done[b], 0), "wait");
+            HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_work, p.out_done[b], 0), "wait");
+            std::vector<uint32_t> counts(ds->n, 0);
+            rc = aqz_ds_run_device_batch(ds, p.d_in[b], g, p.d_out[b].data(),
+                                         counts.data(), p.s_work);
+            if (rc)
+                return drain(rc);
+            HIP_TRY_DRAIN(ds, hipEventRecord(p.work_done[b], p.s_work), "event");
+            // download every frame this group emitted, appended per level
+            HIP_TRY_DRAIN(ds, hipStreamWaitEvent(p.s_out, p.work_done[b], 0), "wait");
+            for (uint32_t l = 1; l < ds->n; ++l) {
+                if (!counts[l])
+                    continue;
+                uint8_t* dst = static_cast<uint8_t*>(host_out_levels[l]) +
+                               size_t(total[l]) * ds->bytes[l];
+                HIP_TRY_DRAIN(ds,
+                        hipMemcpyAsync(dst, p.d_out[b][l], size_t(counts[l]) * ds->bytes[l],
+                                       hipMemcpyDeviceToHost, p.s_out),
+                        "hipMemcpyAsync D2H");
+                total[l] += counts[l];
+            }
+            HIP_TRY_DRAIN(ds, hipEventRecord(p.out_done[b], p.s_out), "event");
         }
-        HIP_TRY_DRAIN(ds, hipEventRecord(p.out_done[b], p.s_out), "event");
+        drain(AQZ_OK);
+        total[0] = n_frames;
+        if (out_counts)
+            std::copy(total.begin(), total.end(), out_counts);
+        return rc;
+    #undef HIP_TRY_DRAIN
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
     }
-    drain(AQZ_OK);
-    total[0] = n_frames;
-    if (out_counts)
-        std::copy(total.begin(), total.end(), out_counts);
-    return rc;
-#undef HIP_TRY_DRAIN
 }
 
 int
