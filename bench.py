@@ -331,6 +331,16 @@ def main():
                                                           args.e2e_frames, device,
                                                           args.sink)
 
+    if world > 1 and args.e2e_frames > 0:
+        # host-to-host on every GPU at once: each rank over its own PCIe link
+        nmulti = min(B, 32)
+        e2e_multi = measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, nmulti,
+                                          device, dist, dev)
+        e2e_multi["value"] = round(e2e_multi["value"] * world, 3)
+        e2e_multi["pcie_GBps"] = round(e2e_multi["pcie_GBps"] * world, 1)
+        e2e_multi["path"] += f", all {world} ranks at once (aggregate, max-over-ranks time)"
+        e2e = {"pipelined_all_ranks": e2e_multi}
+
     if rank == 0:
         metric = HEADLINE_METRIC if args.workload == "4096x4096_u16" else (
             f"GPixels/s device-resident multiscale downsample, {args.workload}, "
@@ -732,10 +742,13 @@ def measure_e2e_sink(aqz, geo, dtype, method, n_frames, device, sink_dir):
             "path": "add_frame + take_frame + writer thread -> per-level raw files, fsync"}
 
 
-def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device):
+def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device, dist=None,
+                          dev="cpu"):
     """Host-resident frames through aqz_ds_run_host_batch: pinned input and
     level buffers, upload / kernels / download overlapped in double-buffered
-    groups — the PCIe-inclusive rate a caller that overlaps frames gets."""
+    groups — the PCIe-inclusive rate a caller that overlaps frames gets.
+    With `dist`, every rank runs it at once (each GPU over its own PCIe link)
+    between barriers and the time is the max over ranks."""
     W, H, _ = geo[0]
     bpp = np.dtype(dtype).itemsize
     src = d_in[:n * W * H * bpp].cpu().pin_memory()
@@ -746,9 +759,11 @@ def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device):
     ds.run_host_batch(src.data_ptr(), n, ptrs)  # warm: allocates the pipeline
     best = None
     for _ in range(3):
+        if dist is not None:
+            dist.barrier()
         t0 = time.perf_counter()
         ds.run_host_batch(src.data_ptr(), n, ptrs)
-        el = time.perf_counter() - t0
+        el = max_over_ranks(time.perf_counter() - t0, dist, dev)
         best = el if best is None else min(best, el)
     ds.close()
     in_bytes = n * W * H * bpp
