@@ -29,6 +29,16 @@ namespace {
 // Native 16-byte vector (HIP's uint4 is a struct; the builtins want this).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// The same widths at byte alignment, for the fused kernels' frame accesses:
+// a batch of odd-width frames puts rows (and frames) at any byte offset.
+// gfx950 global loads/stores take unaligned addresses (the compiler emits the
+// same global_load_dwordx4 / global_store_dwordx2 for these types); the
+// bytes a wave touches are unchanged, so HBM traffic is unchanged.
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+typedef uint64_t u64_u __attribute__((aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+typedef uint16_t u16_u __attribute__((aligned(1)));
+
 enum
 {
     kDecimate = 0,
@@ -130,18 +140,7 @@ shfl_down_any(T v, int delta)
     }
 }
 
-template<bool NT, typename Q>
-__device__ __forceinline__ void
-store_q(Q* dst, Q q)
-{
-    if constexpr (NT) {
-        __builtin_nontemporal_store(q, dst);
-    } else {
-        *dst = q;
-    }
-}
-
-// Store N contiguous elements of T as one naturally aligned access
+// Store N contiguous elements of T as one access at any byte alignment
 // (optionally non-temporal: write-once pyramid levels).
 template<typename T, int N, bool NT = false>
 __device__ __forceinline__ void
@@ -152,24 +151,76 @@ store_vec(T* dst, const T (&v)[N])
     if constexpr (B == 16) {
         u32x4 q;
         __builtin_memcpy(&q, v, 16);
-        store_q<NT>(reinterpret_cast<u32x4*>(dst), q);
+        u32x4_u* d = reinterpret_cast<u32x4_u*>(dst); // typedef keeps align 1
+        if constexpr (NT)
+            __builtin_nontemporal_store(q, d);
+        else
+            *d = q;
     } else if constexpr (B == 8) {
         uint64_t q;
         __builtin_memcpy(&q, v, 8);
-        store_q<NT>(reinterpret_cast<uint64_t*>(dst), q);
+        u64_u* d = reinterpret_cast<u64_u*>(dst); // typedef keeps align 1
+        if constexpr (NT)
+            __builtin_nontemporal_store(q, d);
+        else
+            *d = q;
     } else if constexpr (B == 4) {
         uint32_t q;
         __builtin_memcpy(&q, v, 4);
-        store_q<NT>(reinterpret_cast<uint32_t*>(dst), q);
+        u32_u* d = reinterpret_cast<u32_u*>(dst); // typedef keeps align 1
+        if constexpr (NT)
+            __builtin_nontemporal_store(q, d);
+        else
+            *d = q;
     } else if constexpr (B == 2) {
         uint16_t q;
         __builtin_memcpy(&q, v, 2);
-        store_q<NT>(reinterpret_cast<uint16_t*>(dst), q);
+        u16_u* d = reinterpret_cast<u16_u*>(dst); // typedef keeps align 1
+        if constexpr (NT)
+            __builtin_nontemporal_store(q, d);
+        else
+            *d = q;
     } else {
         uint8_t q;
         __builtin_memcpy(&q, v, 1);
-        store_q<NT>(reinterpret_cast<uint8_t*>(dst), q);
+        uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+        if constexpr (NT)
+            __builtin_nontemporal_store(q, d);
+        else
+            *d = q;
     }
+}
+
+// E elements of T from row `row` starting at column `col`, as one LB-byte
+// load (any alignment).  EDGE: rows past the frame (`row_ok` false) and
+// chunks starting at or past `W` read as zero.  A chunk straddling the row
+// end is still one vector load when `tail_safe` (the bytes past the row end
+// belong to the next row or frame of the same buffer; the kernel replaces
+// those columns by edge replication anyway), else — the last row of the
+// last frame — element by element, so nothing outside the buffer is read.
+template<typename T, int E, bool NT, bool EDGE>
+__device__ __forceinline__ void
+load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tail_safe)
+{
+    constexpr int LB = E * int(sizeof(T));
+    static_assert(LB == 16 || LB == 8, "fused loads are 8 or 16 bytes");
+    if (!EDGE || (row_ok && col < W && (tail_safe || col + E <= W))) {
+        // explicit byte-aligned pointer types (a template argument would drop
+        // the typedef's alignment)
+        if constexpr (LB == 16) {
+            const u32x4_u* a = reinterpret_cast<const u32x4_u*>(row + col);
+            const u32x4 q = NT ? __builtin_nontemporal_load(a) : *a;
+            __builtin_memcpy(out, &q, 16);
+        } else {
+            const u64_u* a = reinterpret_cast<const u64_u*>(row + col);
+            const uint64_t q = NT ? __builtin_nontemporal_load(a) : *a;
+            __builtin_memcpy(out, &q, 8);
+        }
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        out[e] = (row_ok && col + e < W) ? row[col + e] : T(0);
 }
 
 // ---- fused cascade ---------------------------------------------------------
@@ -281,9 +332,20 @@ store_level(T* dst,
         if constexpr (EDGE) {
             ok = ok && (rout0 + r < hout) && (cout0 < wout);
         }
-        if (ok) {
-            store_vec<T, CO, NTS>(dst + uint64_t(rout0 + r) * wout + cout0,
-                                  out[r]);
+        if (!ok)
+            continue;
+        T* d = dst + uint64_t(rout0 + r) * wout + cout0;
+        if (!EDGE || cout0 + CO <= wout) {
+            store_vec<T, CO, NTS>(d, out[r]);
+        } else {
+            // the lane's block overhangs the row end (any-width frames)
+#pragma unroll
+            for (int c = 0; c < CO; ++c) {
+                if (cout0 + c < wout) {
+                    const T one[1] = { out[r][c] };
+                    store_vec<T, 1, NTS>(d + c, one);
+                }
+            }
         }
     }
 }
@@ -334,34 +396,21 @@ cascade_unit(const CascadeParams& p,
     constexpr int LB = RB >= 16 ? 16 : RB;   // bytes per load (8 for narrow tiles)
     constexpr int V = RB / LB;               // loads per row
     constexpr int E = LB / int(sizeof(T));   // elements per load
-    static_assert(LB == 16 || LB == 8, "cascade loads are 8 or 16 bytes");
-    using LoadT = std::conditional_t<LB == 16, u32x4, uint64_t>;
     const T* src =
       reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
 
     T v[R][C];
     // All row loads are issued before any arithmetic: 2^NL * V outstanding
     // loads per lane (1 KiB per wave instruction at 16 B).
+    // reading past a row end stays in the buffer except on the batch's last row
+    const bool last_frame = f + 1 == p.total_units / (p.units_x * p.units_y);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
 #pragma unroll
         for (int k = 0; k < V; ++k) {
-            const uint32_t col = col0 + uint32_t(k) * E;
-            bool ok = true;
-            if constexpr (EDGE) {
-                ok = (row0 + r < p.H) && (col < p.W);
-            }
-            LoadT q{};
-            if (ok) {
-                const LoadT* a = reinterpret_cast<const LoadT*>(
-                  src + uint64_t(row0 + r) * p.W + col);
-                if constexpr (NT) {
-                    q = __builtin_nontemporal_load(a);
-                } else {
-                    q = *a;
-                }
-            }
-            __builtin_memcpy(&v[r][k * E], &q, LB);
+            load_chunk<T, E, NT, EDGE>(&v[r][k * E], src + uint64_t(row0 + r) * p.W,
+                                       col0 + uint32_t(k) * E, p.W, row0 + r < p.H,
+                                       !last_frame || row0 + r + 1 < p.H);
         }
     }
     cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS>(p, v, f, row0, col0, lane);
@@ -481,6 +530,7 @@ volume_unit(const VolumeParams& p,
     constexpr int R = 1 << NL;
     constexpr int Z = 1 << NL;
     constexpr int V = C * int(sizeof(T)) / 16;
+    const bool last_group = g + 1 == p.total_units / (p.units_x * p.units_y);
     T v[Z][R][C];
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
@@ -490,17 +540,11 @@ volume_unit(const VolumeParams& p,
         for (int r = 0; r < R; ++r) {
 #pragma unroll
             for (int k = 0; k < V; ++k) {
-                const uint32_t col = col0 + uint32_t(k) * (16 / sizeof(T));
-                bool ok = true;
-                if constexpr (EDGE) {
-                    ok = (row0 + r < p.H) && (col < p.W);
-                }
-                u32x4 q = { 0u, 0u, 0u, 0u };
-                if (ok) {
-                    q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-                      src + uint64_t(row0 + r) * p.W + col));
-                }
-                __builtin_memcpy(&v[z][r][k * (16 / sizeof(T))], &q, 16);
+                constexpr int E = 16 / int(sizeof(T));
+                load_chunk<T, E, true, EDGE>(&v[z][r][k * E], src + uint64_t(row0 + r) * p.W,
+                                             col0 + uint32_t(k) * E, p.W, row0 + r < p.H,
+                                             !(last_group && z == Z - 1) ||
+                                               row0 + r + 1 < p.H);
             }
         }
     }
@@ -942,12 +986,10 @@ cascade_fits(size_t b,
 {
     if (!b || C == 0 || n_out < 1 || n_out > kMaxFusedLevels || W == 0 || H == 0)
         return false;
-    // whole loads per lane (16 B, or 8 B for narrow tiles) from every source
-    // frame of the batch, and a lane never straddles the row end (stores of a
-    // lane's level-J block must stay inside the row)
-    const size_t lb = std::min<size_t>(16, size_t(C) * b);
-    if (W % C != 0 || reinterpret_cast<uintptr_t>(src) % lb != 0 ||
-        (src_frame_elems * b) % lb != 0)
+    // Frames of any width and byte offset: loads and stores take any
+    // alignment, and lanes that straddle a row end work element by element
+    // (load_chunk, store_level).  Only element alignment is required.
+    if (reinterpret_cast<uintptr_t>(src) % b != 0)
         return false;
     uint32_t w = W, h = H;
     for (int i = 0; i < n_out; ++i) {
@@ -955,12 +997,7 @@ cascade_fits(size_t b,
         h = (h + 1) / 2;
         if (outs[i].w != w || outs[i].h != h)
             return false;
-        // level J = i+1 stores max(C*bpp >> J, bpp) bytes per lane; rows are
-        // multiples of that (W % C == 0), so frame base and stride must be too
-        const size_t sw = std::max<size_t>((size_t(C) * b) >> (i + 1), b);
-        if (reinterpret_cast<uintptr_t>(outs[i].ptr) % sw != 0)
-            return false;
-        if ((outs[i].frame_elems * b) % sw != 0)
+        if (reinterpret_cast<uintptr_t>(outs[i].ptr) % b != 0)
             return false;
     }
     return true;
@@ -1105,8 +1142,6 @@ launch_volume(int dtype,
 {
     if (!volume_supported(dtype, src, W, H, outs, n_out) || n_planes == 0 ||
         n_planes % (1u << n_out) != 0)
-        return hipErrorInvalidValue;
-    if ((src_frame_elems * dtype_bytes(dtype)) % 16 != 0)
         return hipErrorInvalidValue;
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);

@@ -173,36 +173,10 @@ BATCH_GEOMETRIES = {
     "2d_narrow_odd": (halving_geometry(520, 301, 3), 5, 1),
     # six levels: a second fused run from a 63 x 38 level
     "2d_six": (halving_geometry(1000, 600, 6), 3, 1),
+    # odd widths at every level, frames at odd byte offsets in the batch
+    "2d_oddw_deep": (halving_geometry(1031, 517, 5), 3, 1),
+    "3d_fused_oddw": ([(201, 61, 8), (101, 31, 4), (51, 16, 2)], 8, 2),
 }
-
-
-def expected_2d_kind(geo, bpp):
-    """Restates cascade_pick_cols / the batch planner: a 2-D batch is kind 1
-    when every run of up to 4 XY levels fits the fused cascade with the wide
-    (16 B per lane, 32 B for 4/8-byte types) or the narrow (half) tile, and
-    kind 3 (the other runs on batched single-level kernels) otherwise."""
-    cw = (32 if bpp >= 4 else 16) // bpp
-    cn = cw // 2
-
-    def fits(L, k, c):
-        W, H, _ = geo[L - 1]
-        lb = min(16, c * bpp)
-        if W % c or (W * H * bpp) % lb:
-            return False
-        for i in range(k):
-            w, h, _ = geo[L + i]
-            sw = max((c * bpp) >> (i + 1), bpp)
-            if (w * h * bpp) % sw:
-                return False
-        return True
-
-    L = 1
-    while L < len(geo):
-        k = min(len(geo) - L, 4)
-        if not (fits(L, k, cw) or fits(L, k, cn)):
-            return 3
-        L += k
-    return 1
 
 
 @pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32, np.int64],
@@ -232,12 +206,9 @@ def test_device_batch_matches_stream(aqz, oracle, dtype, method, geo_kind):
                                  [0] + [o.data_ptr() for o in outs[1:]],
                                  launch_stream())
     torch.cuda.synchronize()
-    # the fused 2-D cascade needs every run to fit a wide or narrow tile; the
-    # volume kernel needs 16-byte rows; anything else goes per-frame
-    if kind == 1:
-        kind = expected_2d_kind(geo, bpp)
-    elif kind == 2 and (w * bpp) % 16 != 0:
-        kind = 0
+    # the fused kernels take frames of any width and byte offset, so every
+    # 2-D batch is one fused path (kind 1), pure 2x2x2 stacks the volume
+    # kernel (kind 2), anything else the per-frame state machine (kind 0)
     assert ds.last_batch_kind() == kind
     for L in expected:
         gw, gh, _ = geo[L]
