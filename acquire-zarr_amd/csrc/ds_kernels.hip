@@ -191,36 +191,68 @@ store_vec(T* dst, const T (&v)[N])
     }
 }
 
+// Shift a little-endian LB-byte vector down by `bytes` (0 <= bytes < LB).
+template<int LB>
+__device__ __forceinline__ void
+shift_down(uint64_t (&q)[LB / 8], uint32_t bytes)
+{
+    const uint32_t n = 8 * bytes;
+    if constexpr (LB == 8) {
+        q[0] = n ? q[0] >> n : q[0];
+    } else {
+        uint64_t lo = q[0], hi = q[1];
+        if (n >= 64) {
+            lo = hi >> (n - 64);
+            hi = 0;
+        } else if (n) {
+            lo = (lo >> n) | (hi << (64 - n));
+            hi >>= n;
+        }
+        q[0] = lo;
+        q[1] = hi;
+    }
+}
+
 // E elements of T from row `row` starting at column `col`, as one LB-byte
-// load (any alignment).  EDGE: rows past the frame (`row_ok` false) and
-// chunks starting at or past `W` read as zero.  A chunk straddling the row
-// end is still one vector load when `tail_safe` (the bytes past the row end
-// belong to the next row or frame of the same buffer; the kernel replaces
-// those columns by edge replication anyway), else — the last row of the
-// last frame — element by element, so nothing outside the buffer is read.
+// vector load at any alignment.  EDGE (tiles that touch the frame's right or
+// bottom edge): rows past the frame (`row_ok` false) and chunks starting at
+// or past `W` read as zero.  A chunk that straddles the row end is loaded
+// whole when the bytes past the row end are still inside the buffer
+// (`tail_safe`: they belong to the next row or frame; the kernel replaces
+// those columns by edge replication anyway).  On the batch's last row it is
+// loaded instead as the row's last E elements and shifted down in registers,
+// so nothing outside the buffer is read.  Needs W >= E (cascade_fits).
+// Every lane issues one vector load either way: no divergent element loads,
+// and the edge path costs the interior path no registers.
 template<typename T, int E, bool NT, bool EDGE>
 __device__ __forceinline__ void
 load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tail_safe)
 {
     constexpr int LB = E * int(sizeof(T));
     static_assert(LB == 16 || LB == 8, "fused loads are 8 or 16 bytes");
-    if (!EDGE || (row_ok && col < W && (tail_safe || col + E <= W))) {
+    uint32_t at = col;
+    bool ok = true;
+    if constexpr (EDGE) {
+        ok = row_ok && col < W;
+        if (col + E > W && !tail_safe)
+            at = W - E;
+    }
+    uint64_t q[LB / 8] = {};
+    if (ok) {
         // explicit byte-aligned pointer types (a template argument would drop
         // the typedef's alignment)
         if constexpr (LB == 16) {
-            const u32x4_u* a = reinterpret_cast<const u32x4_u*>(row + col);
-            const u32x4 q = NT ? __builtin_nontemporal_load(a) : *a;
-            __builtin_memcpy(out, &q, 16);
+            const u32x4_u* a = reinterpret_cast<const u32x4_u*>(row + at);
+            const u32x4 v = NT ? __builtin_nontemporal_load(a) : *a;
+            __builtin_memcpy(q, &v, 16);
         } else {
-            const u64_u* a = reinterpret_cast<const u64_u*>(row + col);
-            const uint64_t q = NT ? __builtin_nontemporal_load(a) : *a;
-            __builtin_memcpy(out, &q, 8);
+            const u64_u* a = reinterpret_cast<const u64_u*>(row + at);
+            q[0] = NT ? __builtin_nontemporal_load(a) : *a;
         }
-        return;
     }
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-        out[e] = (row_ok && col + e < W) ? row[col + e] : T(0);
+    if constexpr (EDGE)
+        shift_down<LB>(q, (col - at) * uint32_t(sizeof(T)));
+    __builtin_memcpy(out, q, LB);
 }
 
 // ---- fused cascade ---------------------------------------------------------
@@ -987,9 +1019,12 @@ cascade_fits(size_t b,
     if (!b || C == 0 || n_out < 1 || n_out > kMaxFusedLevels || W == 0 || H == 0)
         return false;
     // Frames of any width and byte offset: loads and stores take any
-    // alignment, and lanes that straddle a row end work element by element
-    // (load_chunk, store_level).  Only element alignment is required.
-    if (reinterpret_cast<uintptr_t>(src) % b != 0)
+    // alignment; a lane straddling a row end loads one vector (load_chunk)
+    // and stores element by element (store_level).  Needs element-aligned
+    // buffers and a row of at least one load (E elements); narrower frames
+    // take the single-level kernels.
+    const size_t lb = std::min<size_t>(16, size_t(C) * b);
+    if (reinterpret_cast<uintptr_t>(src) % b != 0 || W < lb / b)
         return false;
     uint32_t w = W, h = H;
     for (int i = 0; i < n_out; ++i) {
