@@ -21,6 +21,8 @@
 #include "ds_kernels.hh"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace aqz {
@@ -382,16 +384,62 @@ store_level(T* dst,
     }
 }
 
+// Row-band staging (cascade_band_kernel): levels whose rows split 64-byte
+// DRAM bursts are written to LDS first, so that one workgroup — which owns
+// a whole row band of the frame — stores each level's band as one
+// contiguous span in whole 16-byte chunks.  lds[J-1] maps byte 0 to the
+// span start rounded down to 16 bytes (`head` bytes before the span).
+struct StageCtx
+{
+    uint8_t* lds[kMaxFusedLevels];
+    uint32_t head[kMaxFusedLevels];
+    uint32_t mask; // bit J-1: level J is staged
+};
+
+template<typename T, int C, int J, int RO, int CO, bool EDGE>
+__device__ __forceinline__ void
+stage_level(const StageCtx& sc,
+            const T (&out)[RO][CO],
+            uint32_t wout,
+            uint32_t hout,
+            uint32_t col0,
+            uint32_t row0,
+            uint32_t band_row0,
+            int lane)
+{
+    constexpr int SO = kLaneStride<C, J>;
+    const uint32_t cout0 = col0 >> J;
+    const uint32_t rout0 = row0 >> J;
+    const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
+    uint8_t* base = sc.lds[J - 1] + sc.head[J - 1];
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+        bool ok = leader;
+        if constexpr (EDGE) {
+            ok = ok && (rout0 + r < hout) && (cout0 < wout);
+        }
+        if (!ok)
+            continue;
+        T* d = reinterpret_cast<T*>(base) + uint64_t(rout0 + r - (band_row0 >> J)) * wout + cout0;
+#pragma unroll
+        for (int c = 0; c < CO; ++c) {
+            if (!EDGE || cout0 + c < wout)
+                d[c] = out[r][c];
+        }
+    }
+}
+
 // Level J of the 2-D cascade: reduce, store, recurse to J+1.
 template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
-         bool NTS = false>
+         bool NTS = false, bool STAGED = false>
 __device__ __forceinline__ void
 cascade_level(const CascadeParams& p,
               const T (&in)[RI][CI],
               uint32_t f,
               uint32_t row0,
               uint32_t col0,
-              int lane)
+              int lane,
+              const StageCtx* sc = nullptr)
 {
     constexpr int RO = RI / 2;
     constexpr int CO = (CI >= 2) ? CI / 2 : 1;
@@ -403,11 +451,22 @@ cascade_level(const CascadeParams& p,
                                       row0 >> (J - 1));
     T* dst = reinterpret_cast<T*>(p.dst[J - 1]) +
              uint64_t(f) * p.dst_frame_elems[J - 1];
-    store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
-                                            col0, row0, lane);
+    if constexpr (STAGED) {
+        if ((sc->mask >> (J - 1)) & 1u) {
+            // the band's rows start at row0 - row0 % 2^NL: one band per block
+            stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
+                                               row0 & ~((1u << NL) - 1u), lane);
+        } else {
+            store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
+                                                    col0, row0, lane);
+        }
+    } else {
+        store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
+                                                col0, row0, lane);
+    }
     if constexpr (J < NL) {
-        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE, NTS>(p, out, f, row0,
-                                                            col0, lane);
+        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE, NTS, STAGED>(p, out, f, row0,
+                                                                    col0, lane, sc);
     }
 }
 
@@ -415,13 +474,15 @@ cascade_level(const CascadeParams& p,
 // loads / stores.  Every byte of the pyramid is touched exactly once, so both
 // streams are marked non-temporal: measured on MI355X (tools/microbench.hip,
 // profiles/r01) the headline batch drops from ~530 to ~475 us with NT stores.
-template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true>
+template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true,
+         bool STAGED = false>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
              uint32_t row0,
              uint32_t col0,
-             int lane)
+             int lane,
+             const StageCtx* sc = nullptr)
 {
     constexpr int R = 1 << NL;
     constexpr int RB = C * int(sizeof(T));   // bytes per lane per row
@@ -445,7 +506,7 @@ cascade_unit(const CascadeParams& p,
                                        !last_frame || row0 + r + 1 < p.H);
         }
     }
-    cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS>(p, v, f, row0, col0, lane);
+    cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS, STAGED>(p, v, f, row0, col0, lane, sc);
 }
 
 template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true>
@@ -477,6 +538,91 @@ cascade_kernel(CascadeParams p)
             cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
         }
     }
+}
+
+// Band-staged cascade for frames whose level rows split 64-byte bursts
+// (widths like 2000 or 3000 px): one workgroup per row band of one frame,
+// one wave per column tile (blockDim = 64 * units_x, units_x <= 4).  Staged levels
+// (StageCtx) go to LDS; after one barrier the workgroup writes each staged
+// level's band — consecutive level rows are adjacent in memory — as one span
+// of whole, 16-byte-aligned chunks, so only the span's first and last chunk
+// share bursts with the neighbouring bands.  Partial-burst writes measured
+// 30% slower than whole ones on MI355X (tools/pitchbench.hip).
+template<typename T, int M, int NL, int C>
+__global__ __launch_bounds__(256) void
+cascade_band_kernel(CascadeParams p, uint32_t stage_mask)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t band_lds[];
+    constexpr int R = 1 << NL;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ux = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t uy = blockIdx.x % p.units_y;
+    const uint32_t f = blockIdx.x / p.units_y;
+    const uint32_t row0 = uy * R;
+
+    // LDS regions of the staged levels (same arithmetic in every thread)
+    StageCtx sc{};
+    sc.mask = stage_mask;
+    uint32_t len[kMaxFusedLevels] = {};
+    uint8_t* span[kMaxFusedLevels] = {};
+    uint32_t off = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        if (!((stage_mask >> i) & 1u))
+            continue;
+        const uint32_t r0 = row0 >> (i + 1);
+        const uint32_t rows = min(uint32_t(R >> (i + 1)), p.h[i] - min(r0, p.h[i]));
+        span[i] = p.dst[i] + (uint64_t(f) * p.dst_frame_elems[i] + uint64_t(r0) * p.w[i]) *
+                               sizeof(T);
+        len[i] = rows * p.w[i] * uint32_t(sizeof(T));
+        sc.head[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 15u);
+        sc.lds[i] = band_lds + off;
+        off += (sc.head[i] + len[i] + 15u) & ~15u;
+    }
+
+    const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
+    const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
+    if (interior)
+        cascade_unit<T, M, NL, C, true, false, true, true>(p, f, row0, col0, lane, &sc);
+    else
+        cascade_unit<T, M, NL, C, true, true, true, true>(p, f, row0, col0, lane, &sc);
+    __syncthreads();
+
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        if (!((stage_mask >> i) & 1u) || len[i] == 0)
+            continue;
+        const uint32_t head = sc.head[i];
+        const uint32_t end = head + len[i];
+        const uint32_t chunks = (end + 15u) / 16u;
+        uint8_t* g = span[i] - head;
+        for (uint32_t k = threadIdx.x; k < chunks; k += blockDim.x) {
+            const uint32_t a = k * 16u, b = a + 16u;
+            if (a >= head && b <= end) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(sc.lds[i] + a);
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(g + a));
+            } else {
+                // first / last chunk of the span: only the band's own bytes
+                for (uint32_t x = max(a, head); x < min(b, end); ++x)
+                    g[x] = sc.lds[i][x];
+            }
+        }
+    }
+}
+
+// Bytes of LDS cascade_band_kernel needs for a band (upper bound over
+// bands; 0 if no level is staged).
+inline uint32_t
+band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask)
+{
+    uint64_t total = 0;
+    for (int i = 0; i < n_out; ++i) {
+        if ((stage_mask >> i) & 1u) {
+            const uint64_t rows = uint64_t(1) << (n_out - i - 1);
+            total += (15 + rows * outs[i].w * b + 15) & ~uint64_t(15);
+        }
+    }
+    return total > (1u << 30) ? (1u << 30) : uint32_t(total);
 }
 
 // ---- fused volume (2x2x2, two-stage) ----------------------------------------
@@ -1118,10 +1264,56 @@ launch_cascade(int dtype,
         }
         // 4 waves per block, one tile per wave per iteration.
         const uint32_t grid = grid_for(total, 4, g_cascade_grid_cap);
+        // Band staging when some level's rows are not whole 64-byte bursts
+        // and a row band is at most 4 tiles ($AQZ_BAND_STAGING=0: never).
+        // Wider bands would need bigger workgroups, and a workgroup that
+        // waits for its slowest wave before storing costs more than it saves:
+        // 8- and 16-wave bands measured 30% and 50% slower than 4-wave ones
+        // (profiles/r01/shape_sweep_band.log).
+        uint32_t stage_mask = 0;
+        for (int i = 0; i < n_out; ++i) {
+            const bool whole = (uint64_t(outs[i].w) * sizeof(T)) % 64 == 0 &&
+                               (outs[i].frame_elems * sizeof(T)) % 64 == 0 &&
+                               reinterpret_cast<uintptr_t>(outs[i].ptr) % 64 == 0;
+            if (!whole)
+                stage_mask |= 1u << i;
+        }
+        static const bool band_off = [] {
+            const char* v = std::getenv("AQZ_BAND_STAGING");
+            return v && std::strcmp(v, "0") == 0;
+        }();
+        const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask);
+        const uint32_t band_waves = p.units_x;
+        const bool band = stage_mask && !band_off &&
+                          band_waves <= 4 && lds <= 65536 &&
+                          total < (1ull << 31);
+        const uint32_t bands = p.units_y * n_frames;
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
             auto go = [&](auto ctag) {
                 constexpr int C = decltype(ctag)::value;
+                if (band) {
+                    const dim3 blk(64 * band_waves);
+                    switch (n_out) {
+                        case 1:
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C>), dim3(bands), blk,
+                                               lds, stream, p, stage_mask);
+                            break;
+                        case 2:
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C>), dim3(bands), blk,
+                                               lds, stream, p, stage_mask);
+                            break;
+                        case 3:
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C>), dim3(bands), blk,
+                                               lds, stream, p, stage_mask);
+                            break;
+                        default:
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C>), dim3(bands), blk,
+                                               lds, stream, p, stage_mask);
+                            break;
+                    }
+                    return;
+                }
                 switch (n_out) {
                     case 1:
                         hipLaunchKernelGGL((cascade_kernel<T, M, 1, C>), dim3(grid), dim3(256),
