@@ -147,7 +147,4 @@ hipError_t launch_tile_frame_sliced(int dtype,
                                     uint8_t* slice_flags,
                                     hipStream_t stream);
 
-// Tuning knob for the cascade grid (waves resident per CU × CUs); 0 = auto.
-void set_cascade_grid_cap(uint32_t blocks);
-
 } // namespace aqz

@@ -509,34 +509,35 @@ cascade_unit(const CascadeParams& p,
     cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS, STAGED>(p, v, f, row0, col0, lane, sc);
 }
 
-template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true>
+// HAS_EDGE false: every tile is interior (W a whole number of tiles, H of
+// bands) — the edge path is compiled out, which keeps the kernel lean (the
+// headline frames).
+template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true,
+         bool HAS_EDGE = true>
 __global__ __launch_bounds__(256) void
 cascade_kernel(CascadeParams p)
 {
+    // one tile per wave, the grid covers every tile (no grid-stride loop:
+    // measured 2-4% faster for f32 than the looped form)
     constexpr int R = 1 << NL;
     const int lane = threadIdx.x & 63;
-    const uint32_t wave_in_block =
-      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint32_t nwaves = gridDim.x * waves_per_block;
-
-    for (uint32_t u = blockIdx.x * waves_per_block + wave_in_block;
-         u < p.total_units;
-         u += nwaves) {
-        const uint32_t ux = u % p.units_x;
-        const uint32_t t = u / p.units_x;
-        const uint32_t uy = t % p.units_y;
-        const uint32_t f = t / p.units_y;
-        const uint32_t row0 = uy * R;
-        const uint32_t tile_col0 = ux * (64u * C);
-        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
-        const bool interior =
-          (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
-        if (interior) {
-            cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
-        } else {
-            cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
-        }
+    const uint32_t u =
+      blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (u >= p.total_units)
+        return;
+    const uint32_t ux = u % p.units_x;
+    const uint32_t t = u / p.units_x;
+    const uint32_t uy = t % p.units_y;
+    const uint32_t f = t / p.units_y;
+    const uint32_t row0 = uy * R;
+    const uint32_t tile_col0 = ux * (64u * C);
+    const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+    if constexpr (!HAS_EDGE) {
+        cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
+    } else if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
+        cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
+    } else {
+        cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
     }
 }
 
@@ -729,42 +730,41 @@ volume_unit(const VolumeParams& p,
     volume_level<T, M, C, 1, NL, Z, R, C, EDGE, true>(p, v, g, row0, col0, lane);
 }
 
-template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool ZFAST = false>
+// ZFAST puts the plane group innermost in the unit order; HAS_EDGE as
+// cascade_kernel.
+template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool ZFAST = false,
+         bool HAS_EDGE = true>
 __global__ __launch_bounds__(256) void
 volume_kernel(VolumeParams p)
 {
     constexpr int R = 1 << NL;
     const int lane = threadIdx.x & 63;
-    const uint32_t wave_in_block =
-      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint32_t nwaves = gridDim.x * waves_per_block;
-    const uint32_t groups = p.total_units / (p.units_x * p.units_y);
-    for (uint32_t u = blockIdx.x * waves_per_block + wave_in_block;
-         u < p.total_units;
-         u += nwaves) {
-        uint32_t ux, uy, g;
-        if constexpr (ZFAST) {
-            g = u % groups;
-            const uint32_t t = u / groups;
-            ux = t % p.units_x;
-            uy = t / p.units_x;
-        } else {
-            ux = u % p.units_x;
-            const uint32_t t = u / p.units_x;
-            uy = t % p.units_y;
-            g = t / p.units_y;
-        }
-        const uint32_t row0 = uy * R;
-        const uint32_t tile_col0 = ux * (64u * C);
-        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
-        const bool interior =
-          (tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H);
-        if (interior) {
-            volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
-        } else {
-            volume_unit<T, M, NL, C, true>(p, g, row0, col0, lane);
-        }
+    const uint32_t u =
+      blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (u >= p.total_units)
+        return;
+    uint32_t ux, uy, g;
+    if constexpr (ZFAST) {
+        const uint32_t groups = p.total_units / (p.units_x * p.units_y);
+        g = u % groups;
+        const uint32_t t = u / groups;
+        ux = t % p.units_x;
+        uy = t / p.units_x;
+    } else {
+        ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        uy = t % p.units_y;
+        g = t / p.units_y;
+    }
+    const uint32_t row0 = uy * R;
+    const uint32_t tile_col0 = ux * (64u * C);
+    const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+    if constexpr (!HAS_EDGE) {
+        volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
+    } else if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
+        volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
+    } else {
+        volume_unit<T, M, NL, C, true>(p, g, row0, col0, lane);
     }
 }
 
@@ -1093,7 +1093,6 @@ with_method(int method, F&& f)
     }
 }
 
-uint32_t g_cascade_grid_cap = 0;
 
 uint32_t
 grid_for(uint64_t work_items, uint32_t per_block, uint32_t cap)
@@ -1143,11 +1142,6 @@ method_valid(int method)
     return method >= kDecimate && method <= kMax;
 }
 
-void
-set_cascade_grid_cap(uint32_t blocks)
-{
-    g_cascade_grid_cap = blocks;
-}
 
 namespace {
 
@@ -1263,7 +1257,7 @@ launch_cascade(int dtype,
             p.h[i] = outs[i].h;
         }
         // 4 waves per block, one tile per wave per iteration.
-        const uint32_t grid = grid_for(total, 4, g_cascade_grid_cap);
+        const uint32_t grid = grid_for(total, 4, 0);
         // Band staging when some level's rows are not whole 64-byte bursts
         // and a row band is at most 4 tiles ($AQZ_BAND_STAGING=0: never).
         // Wider bands would need bigger workgroups, and a workgroup that
@@ -1314,22 +1308,29 @@ launch_cascade(int dtype,
                     }
                     return;
                 }
+                const bool edges = W % (64u * C) != 0 || H % R != 0;
+                auto launch = [&](auto with_edges, auto without_edges) {
+                    if (edges)
+                        hipLaunchKernelGGL(with_edges, dim3(grid), dim3(256), 0, stream, p);
+                    else
+                        hipLaunchKernelGGL(without_edges, dim3(grid), dim3(256), 0, stream, p);
+                };
                 switch (n_out) {
                     case 1:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C>), dim3(grid), dim3(256),
-                                           0, stream, p);
+                        launch(cascade_kernel<T, M, 1, C, true, true>,
+                               cascade_kernel<T, M, 1, C, true, false>);
                         break;
                     case 2:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C>), dim3(grid), dim3(256),
-                                           0, stream, p);
+                        launch(cascade_kernel<T, M, 2, C, true, true>,
+                               cascade_kernel<T, M, 2, C, true, false>);
                         break;
                     case 3:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C>), dim3(grid), dim3(256),
-                                           0, stream, p);
+                        launch(cascade_kernel<T, M, 3, C, true, true>,
+                               cascade_kernel<T, M, 3, C, true, false>);
                         break;
                     default:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C>), dim3(grid), dim3(256),
-                                           0, stream, p);
+                        launch(cascade_kernel<T, M, 4, C, true, true>,
+                               cascade_kernel<T, M, 4, C, true, false>);
                         break;
                 }
             };
@@ -1395,12 +1396,19 @@ launch_volume(int dtype,
         const uint32_t grid = grid_for(total, 4, 0);
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
+            const bool edges = W % (64u * C) != 0 || H % R != 0;
+            auto launch = [&](auto with_edges, auto without_edges) {
+                if (edges)
+                    hipLaunchKernelGGL(with_edges, dim3(grid), dim3(256), 0, stream, p);
+                else
+                    hipLaunchKernelGGL(without_edges, dim3(grid), dim3(256), 0, stream, p);
+            };
             if (n_out == 1)
-                hipLaunchKernelGGL((volume_kernel<T, M, 1>), dim3(grid),
-                                   dim3(256), 0, stream, p);
+                launch(volume_kernel<T, M, 1, int(C), false, true>,
+                       volume_kernel<T, M, 1, int(C), false, false>);
             else
-                hipLaunchKernelGGL((volume_kernel<T, M, 2>), dim3(grid),
-                                   dim3(256), 0, stream, p);
+                launch(volume_kernel<T, M, 2, int(C), false, true>,
+                       volume_kernel<T, M, 2, int(C), false, false>);
             return hipGetLastError();
         });
     });

@@ -105,6 +105,37 @@ cascade_multi(CascadeParams p)
     }
 }
 
+// 2-D, one tile per wave, frame index fastest in the unit order (waves in
+// flight spread over every frame of the batch instead of one frame's bands)
+template<typename T, int C>
+__global__ __launch_bounds__(256) void
+cascade_frame_fast(CascadeParams p, uint32_t n_frames)
+{
+    constexpr int NL = 4, R = 16;
+    constexpr int V = C * int(sizeof(T)) / 16;
+    constexpr int E = 16 / int(sizeof(T));
+    const int lane = threadIdx.x & 63;
+    const uint32_t u = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (u >= p.total_units)
+        return;
+    const uint32_t f = u % n_frames;
+    const uint32_t t = u / n_frames;
+    const uint32_t ux = t % p.units_x;
+    const uint32_t row0 = (t / p.units_x) * R;
+    const T* src = reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
+    const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
+    T v[R][C];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+              src + uint64_t(row0 + r) * p.W + col0 + k * E));
+            __builtin_memcpy(&v[r][k * E], &q, 16);
+        }
+    cascade_level<T, kMean, C, 1, NL, R, C, false, true>(p, v, f, row0, col0, lane);
+}
+
 // 3-D (NL = 2): U adjacent column tiles per wave
 template<int C, int U>
 __global__ __launch_bounds__(256) void
@@ -329,6 +360,11 @@ main(int argc, char** argv)
         C2D(uint16_t, 8, 1);
         C2D(uint16_t, 8, 2);
         C2D(uint16_t, 16, 1);
+        vs.push_back({ "C8 frame-fastest", alg, [&] {
+                          CascadeParams p = cparams(8);
+                          hipLaunchKernelGGL((cascade_frame_fast<uint16_t, 8>),
+                                             dim3((p.total_units + 3) / 4), dim3(256), 0, 0, p, B);
+                      }, true, {} });
     }
     // ceilings of the same byte mix
     vs.push_back({ "ceiling read", in_bytes, [&] {
