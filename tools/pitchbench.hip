@@ -104,7 +104,8 @@ main(int argc, char** argv)
                                              buf, pitch, segs, bands);
                       }, {} });
     }
-    for (uint32_t pitch : { 4096u, 4352u, 4224u, 4032u, 4064u, 4080u, 4000u }) {
+    for (uint32_t pitch : { 4096u, 4352u, 4224u, 4032u, 4064u, 4080u, 4000u, 8192u, 8320u,
+                            8448u, 8704u, 12288u, 16384u, 16512u }) {
         const uint32_t segs = (pitch + 1023) / 1024;
         const uint32_t bands = uint32_t(bytes / (uint64_t(pitch) * 16));
         const uint64_t moved = uint64_t(bands) * 16 * (pitch / 16 * 16);
