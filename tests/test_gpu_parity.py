@@ -176,6 +176,10 @@ BATCH_GEOMETRIES = {
     # odd widths at every level, frames at odd byte offsets in the batch
     "2d_oddw_deep": (halving_geometry(1031, 517, 5), 3, 1),
     "3d_fused_oddw": ([(201, 61, 8), (101, 31, 4), (51, 16, 2)], 8, 2),
+    # level rows that split 64-B bursts: band-staged stores when a row band
+    # is <= 4 tiles (u8 here), direct stores for wider bands (u16, f32, i64)
+    "2d_wide_misaligned": (halving_geometry(2600, 70, 4), 3, 1),
+    "2d_band_staged": (halving_geometry(1500, 90, 4), 3, 1),
 }
 
 
