@@ -353,7 +353,9 @@ int aqz_ds_run_host_batch(aqz_ds* ds,
  * Diagnostic: the path the last aqz_ds_run_device_batch took —
  * 0 = per-frame state machine, 1 = fused 2-D cascade, 2 = fused volume
  * (XY + Z), 3 = 2-D batch with some level runs on batched single-level
- * kernels (widths or alignments the fused cascade cannot take), -1 = none.
+ * kernels (frames narrower than one 16-byte load, or buffers that are not
+ * element-aligned; the fused kernels take any other width and offset),
+ * -1 = none.
  */
 int aqz_ds_last_batch_kind(const aqz_ds* ds);
 
