@@ -506,6 +506,9 @@ cascade_unit(const CascadeParams& p,
                                        !last_frame || row0 + r + 1 < p.H);
         }
     }
+    // keep every load above the reductions (the scheduler would otherwise
+    // hold back the last rows' loads to save registers)
+    __builtin_amdgcn_sched_barrier(0);
     cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS, STAGED>(p, v, f, row0, col0, lane, sc);
 }
 
