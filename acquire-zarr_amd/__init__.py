@@ -40,6 +40,7 @@ EXPORTS = (
     "aqz_blosc_filter_device", "aqz_crc32c_device", "aqz_tile_slices",
     "aqz_tile_frame_device_sliced",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
+    "aqz_ds_device",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
 )
@@ -116,6 +117,8 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_level_count.restype = u32
     L.aqz_ds_device_memory_usage.argtypes = [vp]
     L.aqz_ds_device_memory_usage.restype = sz
+    L.aqz_ds_device.argtypes = [vp]
+    L.aqz_ds_device.restype = i32
     L.aqz_ds_last_error.argtypes = [vp]
     L.aqz_ds_last_error.restype = ctypes.c_char_p
     L.aqz_last_error.argtypes = []
@@ -282,6 +285,10 @@ class Downsampler:
 
     def device_memory_usage(self) -> int:
         return lib().aqz_ds_device_memory_usage(self._h)
+
+    def device(self) -> int:
+        """HIP ordinal the handle runs on."""
+        return lib().aqz_ds_device(self._h)
 
     def add_frame(self, frame: np.ndarray):
         frame = np.ascontiguousarray(frame)

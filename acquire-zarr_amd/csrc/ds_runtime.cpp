@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -709,13 +710,26 @@ aqz_ds_create(const aqz_level_desc* levels,
             }
         }
 
+        int n_devices = 0;
+        if (hipGetDeviceCount(&n_devices) != hipSuccess)
+            n_devices = 0;
         if (device < 0) {
             const char* env = std::getenv("AQZ_GPU_DEVICE");
-            if (env && *env) {
+            if (env && std::strcmp(env, "spread") == 0) {
+                // each new handle on the next GPU: the arrays of a stream (or
+                // several streams in one process) spread their pyramids over
+                // the node; their frames are independent, so no collective
+                static std::atomic<uint32_t> next{ 0 };
+                device = n_devices > 0 ? int(next++ % uint32_t(n_devices)) : 0;
+            } else if (env && *env) {
                 device = std::atoi(env);
             } else if (hipGetDevice(&device) != hipSuccess) {
                 device = 0;
             }
+        }
+        if (n_devices > 0 && (device < 0 || device >= n_devices)) {
+            set_global_error("create: no HIP device %d (%d visible)", device, n_devices);
+            return AQZ_INVALID_ARGUMENT;
         }
 
         auto* ds = new aqz_ds();
@@ -1479,6 +1493,12 @@ uint32_t
 aqz_ds_level_count(const aqz_ds* ds)
 {
     return ds ? ds->n : 0;
+}
+
+int
+aqz_ds_device(const aqz_ds* ds)
+{
+    return ds ? ds->device : -1;
 }
 
 size_t

@@ -129,6 +129,10 @@ typedef struct aqz_ds aqz_ds;
  * Replaces the constructor `Downsampler(config, method)` (downsampler.cpp:
  * 249-304): dtype and method are validated here.  `device` is the HIP
  * ordinal; -1 selects $AQZ_GPU_DEVICE or else the current device.
+ * $AQZ_GPU_DEVICE=spread gives each new handle the next visible GPU in turn,
+ * so the multiscale arrays of one process spread over a node's GPUs (their
+ * frames are independent: no collective).  An ordinal that names no visible
+ * device is AQZ_INVALID_ARGUMENT.
  * Allocates all device buffers and pinned staging up front.
  */
 int aqz_ds_create(const aqz_level_desc* levels,
@@ -358,6 +362,9 @@ int aqz_ds_run_host_batch(aqz_ds* ds,
  * -1 = none.
  */
 int aqz_ds_last_batch_kind(const aqz_ds* ds);
+
+/* HIP ordinal the handle runs on (-1 for a null handle). */
+int aqz_ds_device(const aqz_ds* ds);
 
 /* Bytes of one frame at `level` (0 on bad level). */
 size_t aqz_ds_level_bytes(const aqz_ds* ds, uint32_t level);

@@ -723,3 +723,34 @@ def test_input_frame_take_and_batch_rules(aqz, oracle):
         ds.take_input_frame(16, 0)
     ds.set_input_transpose(False)
     ds.close()
+
+
+# ---- device placement ------------------------------------------------------
+
+def test_spread_device_policy(aqz, oracle, monkeypatch):
+    """$AQZ_GPU_DEVICE=spread: handles take the visible GPUs in turn (all 0
+    on a one-GPU box) and each computes the right pyramid there."""
+    torch = torch_cuda()
+    n_dev = torch.cuda.device_count()
+    monkeypatch.setenv("AQZ_GPU_DEVICE", "spread")
+    geo = halving_geometry(96, 64, 3)
+    rng = np.random.default_rng(seed_of("spread"))
+    handles = [aqz.Downsampler(geo, np.uint16, aqz.MEAN) for _ in range(3)]
+    devices = [h.device() for h in handles]
+    assert all(0 <= d < n_dev for d in devices)
+    if n_dev > 1:
+        assert len(set(devices)) > 1
+    for h in handles:
+        frame = random_frames(rng, np.uint16, (64, 96))
+        h.add_frame(frame)
+        ref = oracle.cascade_2d(frame, len(geo), aqz.MEAN)
+        for L in range(1, len(geo)):
+            assert np.array_equal(h.take_frame(L), ref[L - 1])
+        h.close()
+
+
+def test_bad_device_ordinal_is_invalid_argument(aqz):
+    n_dev = torch_cuda().cuda.device_count()
+    with pytest.raises(aqz.AqzError) as e:
+        aqz.Downsampler(halving_geometry(64, 64, 2), np.uint8, aqz.MEAN, device=n_dev + 7)
+    assert e.value.status == 1  # AQZ_INVALID_ARGUMENT
