@@ -25,6 +25,7 @@ namespace aqz {
 namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_u __attribute__((aligned(1))); // any byte alignment (gfx950 global loads)
 
 // A run of equally sized blocks: block g of the run starts at
 // (g / per) * stride + first + (g % per) * bs.  A launch covers blocks
@@ -348,8 +349,6 @@ filter_run(int shuffle, uint32_t ts, const uint8_t* src, uint8_t* dst, const Blo
 // ---- crc32c -----------------------------------------------------------------
 
 constexpr uint32_t kCrc32cPoly = 0x82F63B78u; // reflected Castagnoli
-constexpr int kCrcThreads = 1024;
-constexpr int kCrcLevels = 10; // log2(kCrcThreads)
 
 // a * b mod P over GF(2), reflected bit order (zlib's multmodp), branch-free
 __host__ __device__ inline uint32_t
@@ -380,83 +379,102 @@ x8nmodp(uint64_t n)
     return p;
 }
 
-struct LevelPow
+// Shift tables for crc32c_kernel, passed by value as a kernel argument.
+constexpr int kCrcThreadsPerWg = 256;
+constexpr uint32_t kCrcSeg = 64;                                  // bytes per thread
+constexpr uint32_t kCrcWgBytes = kCrcThreadsPerWg * kCrcSeg;      // 16 KiB per workgroup
+constexpr int kCrcWgLevels = 16;                                  // up to 2^16 workgroups a buffer
+
+struct CrcPow
 {
-    uint32_t v[kCrcLevels]; // x^(8 * per * 2^level) mod P
+    uint32_t seg[kCrcThreadsPerWg]; // x^(8 * 64 * t) mod P
+    uint32_t wg[kCrcWgLevels];      // x^(8 * 16 KiB * 2^l) mod P
 };
 
-// One workgroup per buffer.  The buffer is cut into kCrcThreads segments of
-// `per` bytes aligned to its END (the first segments short or empty); each
-// thread CRCs its segment (32 byte loads in flight, slicing-by-8 tables in
-// LDS), then segment CRCs are combined pairwise left to right,
-// crc(A||B) = crc(A) * x^(8|B|) ^ crc(B) (zlib's crc32_combine).  With
-// end-aligned segments a right operand is shorter than s*per only when its
-// left operand is empty (crc 0), so the host-computed per-level powers are
-// the only ones ever needed.
-__global__ __launch_bounds__(kCrcThreads) void
-crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride, uint64_t per,
-              LevelPow pw, uint32_t* __restrict__ crcs)
+// CRC-32C of many equal-length buffers, 16 KiB of a buffer per workgroup.
+// The buffer is cut into 64-byte segments aligned to its END; segment j
+// (counted from the end) belongs to thread j % 256 of workgroup j / 256.
+// By linearity of the CRC register update over GF(2):
+//   CRC(M) = R0(M) ^ R_init(0^n) ^ ~0,   R0(M) = XOR_j R0(seg_j) * x^(8*64*j)
+// where R0 is the register after a zero-initialised run (zlib's
+// crc32_combine identity).  Each thread shifts its segment's R0 by its
+// place in the workgroup (one table multiply), the workgroup XOR-reduces
+// them, shifts the result by the workgroup's place (binary powers), and
+// XORs it into crcs[b] atomically; crcs[b] was preset to R_init(0^n) ^ ~0
+// on the host side of the launch.  No ordering between workgroups is
+// needed, so every CU works on a table at once.
+__global__ __launch_bounds__(kCrcThreadsPerWg) void
+crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride, uint32_t wgs,
+              CrcPow pw, uint32_t* __restrict__ crcs)
 {
     __shared__ uint32_t table[8][256];
-    __shared__ uint32_t seg_crc[kCrcThreads];
+    __shared__ uint32_t wave_x[kCrcThreadsPerWg / 64];
     const uint32_t tid = threadIdx.x;
-    if (tid < 256) {
+    {
         uint32_t c = tid;
         for (int k = 0; k < 8; ++k)
             c = (c >> 1) ^ (kCrc32cPoly & (0u - (c & 1u)));
         table[0][tid] = c;
     }
     __syncthreads();
-    if (tid < 256) {
-        for (int k = 1; k < 8; ++k) {
-            const uint32_t prev = table[k - 1][tid];
-            table[k][tid] = (prev >> 8) ^ table[0][prev & 0xFFu];
-        }
+    for (int k = 1; k < 8; ++k) {
+        const uint32_t prev = table[k - 1][tid];
+        table[k][tid] = (prev >> 8) ^ table[0][prev & 0xFFu];
     }
     __syncthreads();
-    const uint8_t* buf = data + uint64_t(blockIdx.x) * stride;
-    const uint64_t from_end0 = per * (kCrcThreads - tid); // start, counted from the end
-    const uint64_t from_end1 = from_end0 - per;
-    const uint64_t b0 = from_end0 < nbytes ? nbytes - from_end0 : 0;
-    const uint64_t b1 = from_end1 < nbytes ? nbytes - from_end1 : 0;
-    uint32_t c = 0xFFFFFFFFu;
-    auto step8 = [&](const uint8_t* b) { // slicing-by-8
-        const uint32_t lo = c ^ (uint32_t(b[0]) | uint32_t(b[1]) << 8 | uint32_t(b[2]) << 16 |
-                                 uint32_t(b[3]) << 24);
+
+    const uint32_t b = blockIdx.x / wgs;
+    const uint32_t q = blockIdx.x % wgs;
+    const uint8_t* buf = data + uint64_t(b) * stride;
+    const uint64_t j = uint64_t(q) * kCrcThreadsPerWg + tid; // segment, from the end
+    uint32_t c = 0;                                          // zero-initialised register
+    auto step8 = [&](const uint8_t* v) {                     // slicing-by-8
+        const uint32_t lo = c ^ (uint32_t(v[0]) | uint32_t(v[1]) << 8 | uint32_t(v[2]) << 16 |
+                                 uint32_t(v[3]) << 24);
         c = table[7][lo & 0xFFu] ^ table[6][(lo >> 8) & 0xFFu] ^ table[5][(lo >> 16) & 0xFFu] ^
-            table[4][lo >> 24] ^ table[3][b[4]] ^ table[2][b[5]] ^ table[1][b[6]] ^
-            table[0][b[7]];
+            table[4][lo >> 24] ^ table[3][v[4]] ^ table[2][v[5]] ^ table[1][v[6]] ^
+            table[0][v[7]];
     };
-    uint64_t i = b0;
-    // whole 32-byte runs: 32 unconditional loads in flight, then 4 steps
-    for (; i + 32 <= b1; i += 32) {
-        uint8_t v[32];
+    if (kCrcSeg * j < nbytes) {
+        const uint64_t end = nbytes - kCrcSeg * j;
+        if (end >= kCrcSeg) {
+            // a whole segment: four 16-byte loads in flight, any alignment
+            // (shard index tables sit at 4-byte offsets after their CRC)
+            const uint8_t* s = buf + end - kCrcSeg;
+            u32x4 w[4];
 #pragma unroll
-        for (int k = 0; k < 32; ++k)
-            v[k] = buf[i + k];
+            for (int k = 0; k < 4; ++k)
+                w[k] = *reinterpret_cast<const u32x4_u*>(s + 16 * k);
+            uint8_t v[64];
+            __builtin_memcpy(v, w, 64);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            step8(v + 8 * q);
+            for (int k = 0; k < 8; ++k)
+                step8(v + 8 * k);
+        } else {
+            // the buffer's first, short segment
+            for (uint64_t i = 0; i < end; ++i)
+                c = (c >> 8) ^ table[0][(c ^ buf[i]) & 0xFFu];
+        }
+        c = multmodp(pw.seg[tid], c); // shift by the segments after it in this workgroup
     }
-    for (; i + 8 <= b1; i += 8) {
-        uint8_t v[8];
+    // XOR over the workgroup
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            v[k] = buf[i + k];
-        step8(v);
-    }
-    for (; i < b1; ++i)
-        c = (c >> 8) ^ table[0][(c ^ buf[i]) & 0xFFu];
-    seg_crc[tid] = c ^ 0xFFFFFFFFu; // CRC-32C of the segment alone (0 if empty)
+    for (int d = 32; d >= 1; d >>= 1)
+        c ^= __shfl_xor(c, d);
+    if ((tid & 63) == 0)
+        wave_x[tid >> 6] = c;
     __syncthreads();
-    int level = 0;
-    for (uint32_t s = 1; s < kCrcThreads; s <<= 1, ++level) {
-        if ((tid % (2 * s)) == 0)
-            seg_crc[tid] = multmodp(pw.v[level], seg_crc[tid]) ^ seg_crc[tid + s];
-        __syncthreads();
+    if (tid == 0) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < kCrcThreadsPerWg / 64; ++k)
+            v ^= wave_x[k];
+        // shift by the workgroups after this one: x^(8 * 16 KiB * q)
+        for (int l = 0; l < kCrcWgLevels; ++l)
+            if ((q >> l) & 1u)
+                v = multmodp(pw.wg[l], v);
+        atomicXor(crcs + b, v);
     }
-    if (tid == 0)
-        crcs[blockIdx.x] = seg_crc[0];
 }
 
 } // namespace
@@ -505,13 +523,26 @@ launch_crc32c(const void* data, uint64_t nbytes, uint64_t stride, uint32_t n_buf
 {
     if (n_buffers == 0 || n_buffers >= (1u << 31))
         return hipErrorInvalidValue;
-    const uint64_t per = ((nbytes + kCrcThreads - 1) / kCrcThreads + 7) & ~uint64_t(7);
-    LevelPow pw;
-    pw.v[0] = x8nmodp(per);
-    for (int l = 1; l < kCrcLevels; ++l)
-        pw.v[l] = multmodp(pw.v[l - 1], pw.v[l - 1]); // x^(8*per*2^l)
-    hipLaunchKernelGGL(crc32c_kernel, dim3(n_buffers), dim3(kCrcThreads), 0, stream,
-                       static_cast<const uint8_t*>(data), nbytes, stride, per, pw, crcs);
+    const uint64_t wgs = (nbytes + kCrcWgBytes - 1) / kCrcWgBytes;
+    if (wgs >= (1ull << kCrcWgLevels) || wgs * n_buffers >= (1ull << 31))
+        return hipErrorInvalidValue;
+    // crcs[b] = R_init(0^n) ^ ~0; the kernel XORs R0(M) in
+    const uint32_t preset = multmodp(x8nmodp(nbytes), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(crcs), int(preset),
+                                     n_buffers, stream);
+    if (e != hipSuccess || wgs == 0)
+        return e;
+    CrcPow pw;
+    const uint32_t seg = x8nmodp(kCrcSeg);
+    pw.seg[0] = 1u << 31; // x^0
+    for (int t = 1; t < kCrcThreadsPerWg; ++t)
+        pw.seg[t] = multmodp(seg, pw.seg[t - 1]);
+    pw.wg[0] = x8nmodp(kCrcWgBytes);
+    for (int l = 1; l < kCrcWgLevels; ++l)
+        pw.wg[l] = multmodp(pw.wg[l - 1], pw.wg[l - 1]);
+    hipLaunchKernelGGL(crc32c_kernel, dim3(uint32_t(wgs * n_buffers)), dim3(kCrcThreadsPerWg), 0,
+                       stream, static_cast<const uint8_t*>(data), nbytes, stride,
+                       uint32_t(wgs), pw, crcs);
     return hipGetLastError();
 }
 
