@@ -512,11 +512,7 @@ cascade_unit(const CascadeParams& p,
     cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS, STAGED>(p, v, f, row0, col0, lane, sc);
 }
 
-// HAS_EDGE false: every tile is interior (W a whole number of tiles, H of
-// bands) — the edge path is compiled out, which keeps the kernel lean (the
-// headline frames).
-template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true,
-         bool HAS_EDGE = true>
+template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true>
 __global__ __launch_bounds__(256) void
 cascade_kernel(CascadeParams p)
 {
@@ -535,9 +531,8 @@ cascade_kernel(CascadeParams p)
     const uint32_t row0 = uy * R;
     const uint32_t tile_col0 = ux * (64u * C);
     const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
-    if constexpr (!HAS_EDGE) {
-        cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
-    } else if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
+    // wave-uniform: interior tiles take the edge-free path
+    if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
         cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
     } else {
         cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
@@ -733,10 +728,8 @@ volume_unit(const VolumeParams& p,
     volume_level<T, M, C, 1, NL, Z, R, C, EDGE, true>(p, v, g, row0, col0, lane);
 }
 
-// ZFAST puts the plane group innermost in the unit order; HAS_EDGE as
-// cascade_kernel.
-template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool ZFAST = false,
-         bool HAS_EDGE = true>
+// ZFAST puts the plane group innermost in the unit order.
+template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool ZFAST = false>
 __global__ __launch_bounds__(256) void
 volume_kernel(VolumeParams p)
 {
@@ -762,9 +755,7 @@ volume_kernel(VolumeParams p)
     const uint32_t row0 = uy * R;
     const uint32_t tile_col0 = ux * (64u * C);
     const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
-    if constexpr (!HAS_EDGE) {
-        volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
-    } else if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
+    if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
         volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
     } else {
         volume_unit<T, M, NL, C, true>(p, g, row0, col0, lane);
@@ -1311,29 +1302,22 @@ launch_cascade(int dtype,
                     }
                     return;
                 }
-                const bool edges = W % (64u * C) != 0 || H % R != 0;
-                auto launch = [&](auto with_edges, auto without_edges) {
-                    if (edges)
-                        hipLaunchKernelGGL(with_edges, dim3(grid), dim3(256), 0, stream, p);
-                    else
-                        hipLaunchKernelGGL(without_edges, dim3(grid), dim3(256), 0, stream, p);
-                };
                 switch (n_out) {
                     case 1:
-                        launch(cascade_kernel<T, M, 1, C, true, true>,
-                               cascade_kernel<T, M, 1, C, true, false>);
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
                         break;
                     case 2:
-                        launch(cascade_kernel<T, M, 2, C, true, true>,
-                               cascade_kernel<T, M, 2, C, true, false>);
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
                         break;
                     case 3:
-                        launch(cascade_kernel<T, M, 3, C, true, true>,
-                               cascade_kernel<T, M, 3, C, true, false>);
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
                         break;
                     default:
-                        launch(cascade_kernel<T, M, 4, C, true, true>,
-                               cascade_kernel<T, M, 4, C, true, false>);
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C>), dim3(grid), dim3(256),
+                                           0, stream, p);
                         break;
                 }
             };
@@ -1399,19 +1383,10 @@ launch_volume(int dtype,
         const uint32_t grid = grid_for(total, 4, 0);
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            const bool edges = W % (64u * C) != 0 || H % R != 0;
-            auto launch = [&](auto with_edges, auto without_edges) {
-                if (edges)
-                    hipLaunchKernelGGL(with_edges, dim3(grid), dim3(256), 0, stream, p);
-                else
-                    hipLaunchKernelGGL(without_edges, dim3(grid), dim3(256), 0, stream, p);
-            };
             if (n_out == 1)
-                launch(volume_kernel<T, M, 1, int(C), false, true>,
-                       volume_kernel<T, M, 1, int(C), false, false>);
+                hipLaunchKernelGGL((volume_kernel<T, M, 1>), dim3(grid), dim3(256), 0, stream, p);
             else
-                launch(volume_kernel<T, M, 2, int(C), false, true>,
-                       volume_kernel<T, M, 2, int(C), false, false>);
+                hipLaunchKernelGGL((volume_kernel<T, M, 2>), dim3(grid), dim3(256), 0, stream, p);
             return hipGetLastError();
         });
     });
