@@ -5,8 +5,9 @@
 //   * cascade   — scale_image<T> (:139-206) applied 1..4 times in one pass:
 //                 each wave reads a 2^NL-row base tile once and writes every
 //                 level of the run; odd edges replicated per level.
-//   * xy_generic — one scale_image<T> level, one output pixel per lane; the
-//                 fallback for widths the vector path cannot tile.
+//   * xy_generic — one scale_image<T> level, one output pixel per lane; used
+//                 by the general state machine and for frames narrower than
+//                 one vector load.
 //   * zpair     — average_two_frames<T> (:208-246), out = f(earlier, current).
 //   * volume    — both of the above fused for pyramids whose levels halve XY
 //                 and Z (3-D stacks): 2^NL planes x 2^NL rows per wave, every
@@ -36,10 +37,10 @@ size_t dtype_bytes(int dtype);
 bool dtype_valid(int dtype);
 bool method_valid(int method);
 
-// True when the fused vector cascade can run the given run of levels: the
-// input width must be a multiple of the per-lane vector (16 bytes of T), all
-// pointers 16-byte aligned and each output level exactly ceil(in/2).
-// Columns per lane the fused cascade would use for this run (0: unsupported).
+// Columns per lane the fused cascade would use for this run of levels (0:
+// unsupported).  Any width and byte offset works as long as the buffers are
+// element-aligned, a row holds at least one 16-byte (narrow tiles: 8-byte)
+// load, and each output level is exactly ceil(in/2) of the one before.
 uint32_t cascade_pick_cols(int dtype,
                            const void* src,
                            uint64_t src_frame_elems,
@@ -90,6 +91,8 @@ hipError_t launch_volume(int dtype,
                          hipStream_t stream);
 
 // One XY level, any width/alignment.
+// (The dtype-dispatching launchers below are defined per build shard in
+// ds_kernels.hip and routed by ds_dispatch.cpp.)
 hipError_t launch_xy_generic(int dtype,
                              int method,
                              const void* src,

@@ -20,6 +20,27 @@
 // from the same pass, so the base frame is read exactly once.
 #include "ds_kernels.hh"
 
+// Build sharding (acquire-zarr_amd/Makefile): the library compiles this file
+// AQZ_SHARDS times; shard k instantiates the kernels of the dtypes whose
+// code % AQZ_SHARDS == k, and its dtype-dispatching launchers are named
+// <launcher>_shard<k>.  ds_dispatch.cpp routes each call to its shard, and
+// shard 0 alone defines the dtype-independent helpers.  The shards compile
+// in parallel: one unit held over a thousand kernel instantiations.  Included
+// directly (the tools/ probes), the file builds unsharded.
+#ifndef AQZ_SHARDS
+#define AQZ_SHARDS 1
+#endif
+#ifndef AQZ_SHARD
+#define AQZ_SHARD 0
+#endif
+#if AQZ_SHARDS > 1
+#define AQZ_CAT2_(a, b) a##b
+#define AQZ_CAT_(a, b) AQZ_CAT2_(a, b)
+#define AQZ_SHARDED(name) AQZ_CAT_(name##_shard, AQZ_SHARD)
+#else
+#define AQZ_SHARDED(name) name
+#endif
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -1043,27 +1064,48 @@ template<typename F>
 hipError_t
 with_dtype(int dtype, F&& f)
 {
+    // only this shard's dtypes are instantiated
     switch (dtype) {
         case 0:
-            return f(uint8_t{});
+            if constexpr (0 % AQZ_SHARDS == AQZ_SHARD)
+                return f(uint8_t{});
+            return hipErrorInvalidValue;
         case 1:
-            return f(uint16_t{});
+            if constexpr (1 % AQZ_SHARDS == AQZ_SHARD)
+                return f(uint16_t{});
+            return hipErrorInvalidValue;
         case 2:
-            return f(uint32_t{});
+            if constexpr (2 % AQZ_SHARDS == AQZ_SHARD)
+                return f(uint32_t{});
+            return hipErrorInvalidValue;
         case 3:
-            return f(uint64_t{});
+            if constexpr (3 % AQZ_SHARDS == AQZ_SHARD)
+                return f(uint64_t{});
+            return hipErrorInvalidValue;
         case 4:
-            return f(int8_t{});
+            if constexpr (4 % AQZ_SHARDS == AQZ_SHARD)
+                return f(int8_t{});
+            return hipErrorInvalidValue;
         case 5:
-            return f(int16_t{});
+            if constexpr (5 % AQZ_SHARDS == AQZ_SHARD)
+                return f(int16_t{});
+            return hipErrorInvalidValue;
         case 6:
-            return f(int32_t{});
+            if constexpr (6 % AQZ_SHARDS == AQZ_SHARD)
+                return f(int32_t{});
+            return hipErrorInvalidValue;
         case 7:
-            return f(int64_t{});
+            if constexpr (7 % AQZ_SHARDS == AQZ_SHARD)
+                return f(int64_t{});
+            return hipErrorInvalidValue;
         case 8:
-            return f(float{});
+            if constexpr (8 % AQZ_SHARDS == AQZ_SHARD)
+                return f(float{});
+            return hipErrorInvalidValue;
         case 9:
-            return f(double{});
+            if constexpr (9 % AQZ_SHARDS == AQZ_SHARD)
+                return f(double{});
+            return hipErrorInvalidValue;
         default:
             return hipErrorInvalidValue;
     }
@@ -1100,6 +1142,7 @@ grid_for(uint64_t work_items, uint32_t per_block, uint32_t cap)
 }
 
 } // namespace
+#if AQZ_SHARD == 0
 
 size_t
 dtype_bytes(int dtype)
@@ -1123,20 +1166,26 @@ dtype_bytes(int dtype)
             return 0;
     }
 }
+#endif
+#if AQZ_SHARD == 0
 
 bool
 dtype_valid(int dtype)
 {
     return dtype_bytes(dtype) != 0;
 }
+#endif
+#if AQZ_SHARD == 0
 
 bool
 method_valid(int method)
 {
     return method >= kDecimate && method <= kMax;
 }
+#endif
 
 
+#if AQZ_SHARD == 0
 namespace {
 
 // Can the fused cascade run this level run with C columns per lane?
@@ -1173,6 +1222,8 @@ cascade_fits(size_t b,
 }
 
 } // namespace
+#endif
+#if AQZ_SHARD == 0
 
 uint32_t
 cascade_pick_cols(int dtype,
@@ -1199,6 +1250,8 @@ cascade_pick_cols(int dtype,
         return cn;
     return wide ? cw : 0;
 }
+#endif
+#if AQZ_SHARD == 0
 
 bool
 cascade_supported(int dtype,
@@ -1211,9 +1264,10 @@ cascade_supported(int dtype,
 {
     return cascade_pick_cols(dtype, src, src_frame_elems, W, H, outs, n_out) != 0;
 }
+#endif
 
 hipError_t
-launch_cascade(int dtype,
+AQZ_SHARDED(launch_cascade)(int dtype,
                int method,
                const void* src,
                uint64_t src_frame_elems,
@@ -1329,6 +1383,7 @@ launch_cascade(int dtype,
         });
     });
 }
+#if AQZ_SHARD == 0
 
 bool
 volume_supported(int dtype,
@@ -1342,9 +1397,10 @@ volume_supported(int dtype,
            cascade_fits(dtype_bytes(dtype), src, uint64_t(W) * H, W, H, outs, n_out,
                         cascade_cols(dtype_bytes(dtype)));
 }
+#endif
 
 hipError_t
-launch_volume(int dtype,
+AQZ_SHARDED(launch_volume)(int dtype,
               int method,
               const void* src,
               uint64_t src_frame_elems,
@@ -1391,6 +1447,7 @@ launch_volume(int dtype,
         });
     });
 }
+#if AQZ_SHARD == 0
 
 uint32_t
 tile_slices(uint32_t tile_rows, uint32_t tile_cols)
@@ -1399,6 +1456,7 @@ tile_slices(uint32_t tile_rows, uint32_t tile_cols)
     const uint64_t tile_elems = uint64_t(tile_rows) * tile_cols;
     return uint32_t(std::min<uint64_t>(64, std::max<uint64_t>(1, tile_elems / 8192)));
 }
+#endif
 
 namespace {
 
@@ -1461,7 +1519,7 @@ launch_tile_impl(int dtype,
 } // namespace
 
 hipError_t
-launch_tile_frame(int dtype,
+AQZ_SHARDED(launch_tile_frame)(int dtype,
                   const void* src,
                   uint32_t W,
                   uint32_t H,
@@ -1476,7 +1534,7 @@ launch_tile_frame(int dtype,
 }
 
 hipError_t
-launch_tile_frame_sliced(int dtype,
+AQZ_SHARDED(launch_tile_frame_sliced)(int dtype,
                          const void* src,
                          uint32_t W,
                          uint32_t H,
@@ -1491,7 +1549,7 @@ launch_tile_frame_sliced(int dtype,
 }
 
 hipError_t
-launch_transpose(int dtype,
+AQZ_SHARDED(launch_transpose)(int dtype,
                  const void* src,
                  uint32_t rows,
                  uint32_t cols,
@@ -1525,7 +1583,7 @@ launch_transpose(int dtype,
 }
 
 hipError_t
-launch_xy_generic(int dtype,
+AQZ_SHARDED(launch_xy_generic)(int dtype,
                   int method,
                   const void* src,
                   uint64_t src_frame_elems,
@@ -1556,7 +1614,7 @@ launch_xy_generic(int dtype,
 }
 
 hipError_t
-launch_zpair(int dtype,
+AQZ_SHARDED(launch_zpair)(int dtype,
              int method,
              void* out,
              const void* earlier,
