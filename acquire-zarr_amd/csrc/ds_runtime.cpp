@@ -38,6 +38,11 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// Pyramids up to this many level bytes are read back eagerly (aqz_ds::eager).
+// (A host memcpy of a larger pyramid would cost more than the round trips
+// it saves)
+constexpr size_t kEagerBytes = size_t(1) << 20;
+
 void
 set_global_error(const char* fmt, ...)
 {
@@ -113,6 +118,16 @@ struct aqz_ds
     void* h_stage = nullptr;
     size_t device_bytes = 0;
     int last_batch_kind = -1;
+
+    // Small pyramids (all levels together <= kEagerBytes): every newly cached
+    // level frame is copied to pinned host memory right behind the kernels,
+    // so the take_frame calls that follow cost one event wait and a memcpy
+    // each instead of a device round trip each ($AQZ_EAGER_READBACK=0: off).
+    bool eager = false;
+    std::vector<uint8_t*> h_level;  // pinned copy per level
+    std::vector<int> host_for;      // slot whose frame h_level holds, -1 none
+    std::vector<uint8_t> no_eager;  // level taken tiled: the host copy would be wasted
+    hipEvent_t levels_d2h = nullptr;
 
     // aqz_ds_take_frame_tiled: on-demand scratch (tiles, then slice flags)
     void* d_tiles = nullptr;
@@ -479,6 +494,30 @@ process_input(aqz_ds* ds, const void* d_frame)
 // Downsampler::add_frame for a host frame: upload it, queue the pyramid, and
 // return once the upload has completed (the caller may then reuse its frame;
 // the kernels are still queued).
+// Queue the D2H of every newly cached level frame into its pinned copy,
+// right behind the kernels that made it (aqz_ds::eager).
+int
+eager_readback(aqz_ds* ds)
+{
+    if (!ds->eager)
+        return AQZ_OK;
+    bool any = false;
+    for (uint32_t L = 1; L < ds->n; ++L) {
+        const int k = ds->cached[L];
+        if (k < 0 || ds->host_for[L] == k || ds->no_eager[L])
+            continue;
+        HIP_TRY(ds,
+                hipMemcpyAsync(ds->h_level[L], ds->slot_ptr(L, k), ds->bytes[L],
+                               hipMemcpyDeviceToHost, ds->stream),
+                "hipMemcpyAsync D2H (eager)");
+        ds->host_for[L] = k;
+        any = true;
+    }
+    if (any)
+        HIP_TRY(ds, hipEventRecord(ds->levels_d2h, ds->stream), "hipEventRecord");
+    return AQZ_OK;
+}
+
 int
 add_host_frame(aqz_ds* ds, const void* host_frame)
 {
@@ -500,6 +539,8 @@ add_host_frame(aqz_ds* ds, const void* host_frame)
     HIP_TRY(ds, hipEventRecord(ds->h2d_done, ds->stream), "hipEventRecord");
     int rc = process_input(ds, ds->d_in);
     if (rc)
+        return rc;
+    if ((rc = eager_readback(ds)) != AQZ_OK)
         return rc;
     if (!ds->staged) {
         // the caller may reuse its frame as soon as we return
@@ -582,6 +623,10 @@ release(aqz_ds* ds)
         (void)hipHostFree(t.second);
     }
     (void)hipHostFree(ds->h_flags);
+    for (uint8_t* h : ds->h_level)
+        (void)hipHostFree(h);
+    if (ds->levels_d2h)
+        (void)hipEventDestroy(ds->levels_d2h);
     (void)hipFree(ds->d_tin);
     if (ds->h2d_done)
         (void)hipEventDestroy(ds->h2d_done);
@@ -752,6 +797,9 @@ aqz_ds_create(const aqz_level_desc* levels,
         ds->tslot.assign(n_levels, { nullptr, nullptr });
         ds->tflags.assign(n_levels, { nullptr, nullptr });
         ds->tiled_for.assign(n_levels, -1);
+        ds->h_level.assign(n_levels, nullptr);
+        ds->host_for.assign(n_levels, -1);
+        ds->no_eager.assign(n_levels, 0);
         for (uint32_t l = 0; l < n_levels; ++l) {
             ds->bytes[l] = size_t(levels[l].width) * levels[l].height * ds->bpp;
             if (l > 0) {
@@ -777,6 +825,21 @@ aqz_ds_create(const aqz_level_desc* levels,
             return fail(e, "hipEventCreate");
         if ((e = hipMalloc(&ds->d_in, ds->bytes[0])) != hipSuccess)
             return fail(e, "hipMalloc level 0");
+        size_t level_total = 0;
+        for (uint32_t l = 1; l < n_levels; ++l)
+            level_total += ds->bytes[l];
+        const char* eager_env = std::getenv("AQZ_EAGER_READBACK");
+        ds->eager = n_levels > 1 && level_total <= kEagerBytes &&
+                    !(eager_env && std::strcmp(eager_env, "0") == 0);
+        if (ds->eager) {
+            if ((e = hipEventCreateWithFlags(&ds->levels_d2h, hipEventDisableTiming)) !=
+                hipSuccess)
+                return fail(e, "hipEventCreate");
+            for (uint32_t l = 1; l < n_levels; ++l)
+                if ((e = hipHostMalloc(reinterpret_cast<void**>(&ds->h_level[l]), ds->bytes[l],
+                                       hipHostMallocDefault)) != hipSuccess)
+                    return fail(e, "hipHostMalloc level copy");
+        }
         if (ds->staged &&
             (e = hipHostMalloc(&ds->h_stage, ds->bytes[0], hipHostMallocDefault)) != hipSuccess)
             return fail(e, "hipHostMalloc staging");
@@ -876,7 +939,9 @@ aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes)
                                 std::to_string(nbytes));
         if (int rc = bind_device(ds))
             return rc;
-        return process_input(ds, device_frame);
+        if (int rc = process_input(ds, device_frame))
+            return rc;
+        return eager_readback(ds);
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
     }
@@ -909,14 +974,21 @@ aqz_ds_take_frame(aqz_ds* ds,
             return ds->fail_arg("take_frame: buffer too small");
         if (int rc = bind_device(ds))
             return rc;
-        // HBM -> caller memory directly (stream-ordered after the kernels)
-        HIP_TRY(ds,
-                hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
-                               ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
-                "hipMemcpyAsync D2H");
-        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        if (ds->eager && ds->host_for[level] == ds->cached[level]) {
+            // already on its way to pinned memory (eager_readback)
+            HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
+            std::memcpy(dst, ds->h_level[level], ds->bytes[level]);
+        } else {
+            // HBM -> caller memory directly (stream-ordered after the kernels)
+            HIP_TRY(ds,
+                    hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
+                                   ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
+                    "hipMemcpyAsync D2H");
+            HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+        }
         ds->cached[level] = -1;
         ds->tiled_for[level] = -1;
+        ds->host_for[level] = -1;
         return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
@@ -948,6 +1020,7 @@ aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t
         tf = { nullptr, nullptr };
         ds->tiling[level] = { 0, 0 };
         ds->tiled_for[level] = -1;
+        ds->no_eager[level] = tile_rows != 0;
         if (tile_rows == 0)
             return AQZ_OK;
         const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
@@ -1012,6 +1085,8 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
         }
         ds->cached[level] = -1;
         ds->tiled_for[level] = -1;
+        ds->host_for[level] = -1;
+        ds->no_eager[level] = 1; // this caller takes the level tiled
         return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
