@@ -618,7 +618,7 @@ def measure_cpu_parallel(geo, dtype, method, seconds, frames, threads):
     W, H, _ = geo[0]
     n_levels = len(geo)
     counts = [0] * threads
-    start = threading.Barrier(threads + 1)
+    start = threading.Barrier(threads + 1, timeout=120)  # a failed worker breaks it
     stop = threading.Event()
 
     def worker(k):
