@@ -402,10 +402,16 @@ struct CrcPow
 // them, shifts the result by the workgroup's place (binary powers), and
 // XORs it into crcs[b] atomically; crcs[b] was preset to R_init(0^n) ^ ~0
 // on the host side of the launch.  No ordering between workgroups is
-// needed, so every CU works on a table at once.
+// needed, so every CU works on a table at once.  A table of at most 16 KiB
+// (Single, the common shard index size) needs no atomic and no preset fill:
+// it gets the next power of two of its segment count in lanes, so small
+// tables pack 256 >> lgp to a workgroup (1 KiB tables: 16), and its first
+// lane stores R0(M) ^ preset after a lane-group XOR.
+template <bool Single>
 __global__ __launch_bounds__(kCrcThreadsPerWg) void
 crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride, uint32_t wgs,
-              CrcPow pw, uint32_t* __restrict__ crcs)
+              uint32_t n_buffers, uint32_t lgp, CrcPow pw, uint32_t preset,
+              uint32_t* __restrict__ crcs)
 {
     __shared__ uint32_t table[8][256];
     __shared__ uint32_t wave_x[kCrcThreadsPerWg / 64];
@@ -423,10 +429,14 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
     }
     __syncthreads();
 
-    const uint32_t b = blockIdx.x / wgs;
-    const uint32_t q = blockIdx.x % wgs;
+    // Single: 2^lgp lanes per table (lgp <= 8), 256 >> lgp tables per workgroup
+    const uint32_t lanes = Single ? (1u << lgp) : uint32_t(kCrcThreadsPerWg);
+    const uint32_t b = Single ? blockIdx.x * (kCrcThreadsPerWg >> lgp) + (tid >> lgp)
+                              : blockIdx.x / wgs;
+    const uint32_t q = Single ? 0u : blockIdx.x % wgs;
+    const uint32_t js = tid & (lanes - 1);                   // segment within the workgroup
     const uint8_t* buf = data + uint64_t(b) * stride;
-    const uint64_t j = uint64_t(q) * kCrcThreadsPerWg + tid; // segment, from the end
+    const uint64_t j = uint64_t(q) * kCrcThreadsPerWg + js; // segment, from the end
     uint32_t c = 0;                                          // zero-initialised register
     auto step8 = [&](const uint8_t* v) {                     // slicing-by-8
         const uint32_t lo = c ^ (uint32_t(v[0]) | uint32_t(v[1]) << 8 | uint32_t(v[2]) << 16 |
@@ -435,7 +445,7 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
             table[4][lo >> 24] ^ table[3][v[4]] ^ table[2][v[5]] ^ table[1][v[6]] ^
             table[0][v[7]];
     };
-    if (kCrcSeg * j < nbytes) {
+    if (b < n_buffers && kCrcSeg * j < nbytes) {
         const uint64_t end = nbytes - kCrcSeg * j;
         if (end >= kCrcSeg) {
             // a whole segment: four 16-byte loads in flight, any alignment
@@ -455,25 +465,37 @@ crc32c_kernel(const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t stride
             for (uint64_t i = 0; i < end; ++i)
                 c = (c >> 8) ^ table[0][(c ^ buf[i]) & 0xFFu];
         }
-        c = multmodp(pw.seg[tid], c); // shift by the segments after it in this workgroup
+        c = multmodp(pw.seg[js], c); // shift by the segments after it in this workgroup
     }
-    // XOR over the workgroup
+    // XOR over each table's lanes (the whole wave when a table spans waves)
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1)
-        c ^= __shfl_xor(c, d);
+    for (uint32_t d = 32; d >= 1; d >>= 1)
+        if (d < lanes)
+            c ^= __shfl_xor(c, d);
+    if (Single && lanes <= 64) {
+        if (js == 0 && b < n_buffers)
+            crcs[b] = c ^ preset;
+        return;
+    }
     if ((tid & 63) == 0)
         wave_x[tid >> 6] = c;
     __syncthreads();
-    if (tid == 0) {
+    const uint32_t wpt = lanes / 64; // waves per table
+    if (tid < kCrcThreadsPerWg / 64 / wpt) {
         uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < kCrcThreadsPerWg / 64; ++k)
-            v ^= wave_x[k];
-        // shift by the workgroups after this one: x^(8 * 16 KiB * q)
-        for (int l = 0; l < kCrcWgLevels; ++l)
-            if ((q >> l) & 1u)
-                v = multmodp(pw.wg[l], v);
-        atomicXor(crcs + b, v);
+        for (uint32_t k = 0; k < wpt; ++k)
+            v ^= wave_x[tid * wpt + k];
+        if constexpr (Single) {
+            const uint32_t bt = blockIdx.x * (kCrcThreadsPerWg >> lgp) + tid;
+            if (bt < n_buffers)
+                crcs[bt] = v ^ preset;
+        } else {
+            // shift by the workgroups after this one: x^(8 * 16 KiB * q)
+            for (int l = 0; l < kCrcWgLevels; ++l)
+                if ((q >> l) & 1u)
+                    v = multmodp(pw.wg[l], v);
+            atomicXor(crcs + b, v);
+        }
     }
 }
 
@@ -528,21 +550,44 @@ launch_crc32c(const void* data, uint64_t nbytes, uint64_t stride, uint32_t n_buf
         return hipErrorInvalidValue;
     // crcs[b] = R_init(0^n) ^ ~0; the kernel XORs R0(M) in
     const uint32_t preset = multmodp(x8nmodp(nbytes), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(crcs), int(preset),
+    if (wgs <= 1) {
+        // empty tables: the CRC is the preset; else one workgroup per table
+        // writes R0(M) ^ preset and nothing needs filling first
+        if (wgs == 0)
+            return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(crcs), int(preset),
                                      n_buffers, stream);
-    if (e != hipSuccess || wgs == 0)
-        return e;
-    CrcPow pw;
-    const uint32_t seg = x8nmodp(kCrcSeg);
-    pw.seg[0] = 1u << 31; // x^0
-    for (int t = 1; t < kCrcThreadsPerWg; ++t)
-        pw.seg[t] = multmodp(seg, pw.seg[t - 1]);
-    pw.wg[0] = x8nmodp(kCrcWgBytes);
-    for (int l = 1; l < kCrcWgLevels; ++l)
-        pw.wg[l] = multmodp(pw.wg[l - 1], pw.wg[l - 1]);
-    hipLaunchKernelGGL(crc32c_kernel, dim3(uint32_t(wgs * n_buffers)), dim3(kCrcThreadsPerWg), 0,
-                       stream, static_cast<const uint8_t*>(data), nbytes, stride,
-                       uint32_t(wgs), pw, crcs);
+    } else {
+        hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(crcs), int(preset),
+                                         n_buffers, stream);
+        if (e != hipSuccess)
+            return e;
+    }
+    // the shift powers do not depend on the launch: computed once
+    static const CrcPow pw = [] {
+        CrcPow p;
+        const uint32_t seg = x8nmodp(kCrcSeg);
+        p.seg[0] = 1u << 31; // x^0
+        for (int t = 1; t < kCrcThreadsPerWg; ++t)
+            p.seg[t] = multmodp(seg, p.seg[t - 1]);
+        p.wg[0] = x8nmodp(kCrcWgBytes);
+        for (int l = 1; l < kCrcWgLevels; ++l)
+            p.wg[l] = multmodp(p.wg[l - 1], p.wg[l - 1]);
+        return p;
+    }();
+    if (wgs == 1) {
+        uint32_t lgp = 0; // lanes per table: next power of two of its segments
+        while ((uint64_t(kCrcSeg) << lgp) < nbytes)
+            ++lgp;
+        const uint32_t per_wg = uint32_t(kCrcThreadsPerWg) >> lgp;
+        hipLaunchKernelGGL(crc32c_kernel<true>, dim3((n_buffers + per_wg - 1) / per_wg),
+                           dim3(kCrcThreadsPerWg), 0, stream,
+                           static_cast<const uint8_t*>(data), nbytes, stride, uint32_t(wgs),
+                           n_buffers, lgp, pw, preset, crcs);
+    } else {
+        hipLaunchKernelGGL(crc32c_kernel<false>, dim3(uint32_t(wgs * n_buffers)),
+                           dim3(kCrcThreadsPerWg), 0, stream, static_cast<const uint8_t*>(data),
+                           nbytes, stride, uint32_t(wgs), n_buffers, 8u, pw, preset, crcs);
+    }
     return hipGetLastError();
 }
 

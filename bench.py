@@ -464,7 +464,15 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
     timed("crc32c_64_index_tables", lambda src, i: aqz.crc32c_device(
         base + (i % ncrc) * tb, 4096 * 16, 4096 * 16 + 4, 64, crcs.data_ptr(), sptr),
         64 * 4096 * 16)
-    raw = d_in[:cbytes * 16].cpu().numpy()
+    # and 1024 tables of 64 chunks (1 KiB each): one workgroup per table,
+    # no preset fill
+    crcs_small = torch.empty(1024, dtype=torch.int32, device="cuda")
+    tbs = 1024 * (64 * 16 + 4)
+    ncrcs = max(1, d_in.numel() // tbs)
+    timed("crc32c_1024_small_index_tables", lambda src, i: aqz.crc32c_device(
+        base + (i % ncrcs) * tbs, 64 * 16, 64 * 16 + 4, 1024, crcs_small.data_ptr(), sptr),
+        1024 * 64 * 16)
+    raw =d_in[:cbytes * 16].cpu().numpy()
     t0 = time.perf_counter()
     for k in range(16):
         orc_mod.blosc_filter(raw[k * cbytes:(k + 1) * cbytes], aqz.BITSHUFFLE, bpp, 65536)

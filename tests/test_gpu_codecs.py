@@ -121,6 +121,24 @@ def test_crc32c_matches_oracle(aqz, oracle, n):
         assert int(got[k]) == oracle.crc32c(host[k * stride:k * stride + n]), f"buffer {k}"
 
 
+@pytest.mark.parametrize("n", [1, 64, 65, 128, 1000, 1024, 4096, 8193, 16384])
+def test_crc32c_packed_small_tables(aqz, oracle, n):
+    """Tables of <= 16 KiB pack 256 >> lgp to a workgroup (lanes = next power
+    of two of their 64-B segments); 37 tables leave a partial last workgroup,
+    and the words after crcs[36] must stay untouched."""
+    torch = torch_cuda()
+    rng = np.random.default_rng(n + 77)
+    nbuf, stride = 37, n + 5
+    host = rng.integers(0, 256, nbuf * stride, dtype=np.uint8)
+    d = to_device(host)
+    out = torch.full((nbuf + 8,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    aqz.crc32c_device(d.data_ptr(), n, stride, nbuf, out.data_ptr(), launch_stream())
+    got = from_device(out, np.uint32, (nbuf + 8,))
+    for k in range(nbuf):
+        assert int(got[k]) == oracle.crc32c(host[k * stride:k * stride + n]), f"buffer {k}"
+    assert all(int(x) == 0x5A5A5A5A for x in got[nbuf:])
+
+
 def test_crc32c_shard_index_tables(aqz, oracle):
     """A batch of shard index tables (Shard::write_table_, shard.cpp:145-166):
     the GPU checksum equals the 4 bytes the reference appends."""
