@@ -1,4 +1,4 @@
-"""CPU, world size 2 over gloo: the multi-GPU bench path's partition and
+"""CPU, world sizes 2 and 4 over gloo: the multi-GPU bench path's partition and
 timing logic (bench.py helpers) — barrier-bracketed timed region, max over
 ranks, whole-job aggregate, and the round-robin frame deal."""
 import os
@@ -58,6 +58,15 @@ def test_two_rank_timing_and_partition():
     assert f0 == [0, 2, 4, 6, 8] and f1 == [1, 3, 5, 7, 9]
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_round_robin_deal_covers_every_frame(world):
+    sys.path.insert(0, ROOT)
+    import bench
+    deals = [list(bench.rank_frames(37, r, world)) for r in range(world)]
+    assert sorted(sum(deals, [])) == list(range(37))
+    assert max(map(len, deals)) - min(map(len, deals)) <= 1
+
+
 def test_aggregate_counts_all_ranks():
     sys.path.insert(0, ROOT)
     import bench
@@ -108,12 +117,16 @@ def _scatter_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_xgmi_scatter_gather_logic():
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_scatter_gather_logic(world):
+    """Rank 0's pool scattered to `world` ranks and the levels gathered back
+    in rank order (4 ranks rehearses the per-peer send loop beyond one peer)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_scatter_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     ok = q.get(timeout=120)
