@@ -283,8 +283,17 @@ def main():
 
     # algorithmic bytes per step: read every input frame once, write every
     # emitted level frame once (counts from the batch call)
-    alg_bytes = B * frame_bytes + sum(counts[L] * geo[L][0] * geo[L][1] * bpp
-                                      for L in range(1, n_levels))
+    # Decimate samples the top-left pixel (and the earlier plane): only the
+    # even rows (and, where level 1 halves Z, the even planes) of the input
+    # are algorithmically needed.  Whole rows, because the sampled columns
+    # share 64-B bursts with the skipped ones.  Every other method reads all.
+    read_bytes = B * frame_bytes
+    if args.method == "decimate" and n_levels > 1:
+        rows = (H + 1) // 2 if geo[1][0] < W or geo[1][1] < H else H
+        planes = (B + 1) // 2 if Z and geo[1][2] < geo[0][2] else B
+        read_bytes = planes * rows * W * bpp
+    alg_bytes = read_bytes + sum(counts[L] * geo[L][0] * geo[L][1] * bpp
+                                 for L in range(1, n_levels))
     kind = ds.last_batch_kind()  # 1 fused 2-D cascade, 2 fused volume, 0 per-frame
     per = {1: 4, 2: 2}.get(kind)  # levels per launch (kind 3: mixed, not derived)
     launches = -(-(n_levels - 1) // per) if per else None
@@ -297,7 +306,7 @@ def main():
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
                 "min_launch_us": round(min(launch_ms) * 1e3, 2)}
 
-    ceiling = measure_ceiling(torch, stream, d_in, B * frame_bytes, alg_bytes - B * frame_bytes,
+    ceiling = measure_ceiling(torch, stream, d_in, read_bytes, alg_bytes - read_bytes,
                               max(5, args.steps // 2))
     if ceiling is not None:
         ceiling["frac_of_ceiling"] = round(achieved / ceiling["GBps"], 4)
@@ -472,7 +481,7 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
     timed("crc32c_1024_small_index_tables", lambda src, i: aqz.crc32c_device(
         base + (i % ncrcs) * tbs, 64 * 16, 64 * 16 + 4, 1024, crcs_small.data_ptr(), sptr),
         1024 * 64 * 16)
-    raw =d_in[:cbytes * 16].cpu().numpy()
+    raw = d_in[:cbytes * 16].cpu().numpy()
     t0 = time.perf_counter()
     for k in range(16):
         orc_mod.blosc_filter(raw[k * cbytes:(k + 1) * cbytes], aqz.BITSHUFFLE, bpp, 65536)
@@ -488,7 +497,7 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
 def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
     """Measured HBM ceiling for the kernel's own byte mix (tools/hbm_probe.hip):
     a contiguous non-temporal stream reading the same input buffer and writing
-    in the nearest of the ratios 12:4, 13:3, 14:2 (4 KiB blocks per
+    in the nearest of the ratios 12:4, 13:3, 14:2, 10:6, 9:7 (4 KiB blocks per
     workgroup), plus a read-only pass, timed with HIP events on the launch
     stream.  A measurement aid, not product code: skipped (None) if the probe
     library was not built."""
@@ -502,7 +511,7 @@ def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     frac_r = read_bytes / max(1, read_bytes + write_bytes)
-    rd, wr = min(((12, 4), (13, 3), (14, 2)), key=lambda m: abs(m[0] / 16 - frac_r))
+    rd, wr = min(((12, 4), (13, 3), (14, 2), (10, 6), (9, 7)), key=lambda m: abs(m[0] / 16 - frac_r))
     dst = torch.empty(read_bytes // rd * wr + 4096, dtype=torch.uint8, device="cuda")
     sink = torch.zeros(16, dtype=torch.uint8, device="cuda")
     out = {}

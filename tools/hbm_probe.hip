@@ -52,7 +52,7 @@ extern "C" {
 
 // Moves blocks * RD * 4 KiB in and blocks * WR * 4 KiB out, blocks =
 // src_bytes / (RD * 4 KiB).  `dst` must hold blocks * WR * 4 KiB; `sink`
-// 4 bytes.  Supported RD:WR = 16:0, 12:4, 13:3, 14:2.  Returns 0 or a
+// 4 bytes.  Supported RD:WR = 16:0, 12:4, 13:3, 14:2, 10:6, 9:7.  Returns 0 or a
 // hipError_t; *moved_bytes = bytes read + written.
 int
 aqz_hbm_probe(const void* src, uint64_t src_bytes, void* dst, void* sink, int rd, int wr,
@@ -75,6 +75,10 @@ aqz_hbm_probe(const void* src, uint64_t src_bytes, void* dst, void* sink, int rd
         hipLaunchKernelGGL((mix_kernel<13, 3>), dim3(blocks), dim3(256), 0, s, in, out, sk);
     else if (rd == 14 && wr == 2)
         hipLaunchKernelGGL((mix_kernel<14, 2>), dim3(blocks), dim3(256), 0, s, in, out, sk);
+    else if (rd == 10 && wr == 6) // Decimate's mix: half the rows read
+        hipLaunchKernelGGL((mix_kernel<10, 6>), dim3(blocks), dim3(256), 0, s, in, out, sk);
+    else if (rd == 9 && wr == 7)
+        hipLaunchKernelGGL((mix_kernel<9, 7>), dim3(blocks), dim3(256), 0, s, in, out, sk);
     else
         return int(hipErrorInvalidValue);
     if (moved_bytes)
