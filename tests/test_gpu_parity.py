@@ -176,6 +176,10 @@ BATCH_GEOMETRIES = {
     # odd widths at every level, frames at odd byte offsets in the batch
     "2d_oddw_deep": (halving_geometry(1031, 517, 5), 3, 1),
     "3d_fused_oddw": ([(201, 61, 8), (101, 31, 4), (51, 16, 2)], 8, 2),
+    # Decimate takes 4 row units per wave when H % 2^NL == 0 and the row
+    # units divide by 4: with column edges, and with one fused level (NL = 1)
+    "3d_fused_oddw_even_h": ([(201, 64, 8), (101, 32, 4), (51, 16, 2)], 8, 2),
+    "3d_fused_one_level": ([(256, 64, 4), (128, 32, 2)], 4, 2),
     # level rows that split 64-B bursts: band-staged stores when a row band
     # is <= 4 tiles (u8 here), direct stores for wider bands (u16, f32, i64)
     "2d_wide_misaligned": (halving_geometry(2600, 70, 4), 3, 1),
