@@ -992,7 +992,8 @@ tile_kernel_vec(const u32x4* __restrict__ src,
 // storage order swaps the two spatial dimensions (Array::write_frame_to_chunks_
 // transposes level 0 before chunking, array.cpp:517-530, and the downsampler
 // then sees the transposed frame).  Pure data movement, HBM-bound:
-// 2 * rows * cols * sizeof(T) bytes.  One block per 64 x 64-element tile,
+// 2 * rows * cols * sizeof(T) bytes.  One block per kTransposeSub tiles of
+// kTransposeTile^2 elements,
 // staged through LDS so both the global reads (source rows) and the global
 // writes (destination rows) are contiguous; with VEC each lane moves 16 B per
 // access on interior tiles.  Edge tiles (and VEC=false frames, whose rows are
@@ -1005,55 +1006,103 @@ constexpr int kTransposeTile = sizeof(T) == 1 ? 128 : 256 / int(sizeof(T));
 template<typename T>
 constexpr int kTransposePitch = kTransposeTile<T> + (sizeof(T) >= 4 ? 1 : 4 / int(sizeof(T)));
 
+// tiles per block, stacked along the source rows: 32 KiB per block for every
+// dtype (a lone 64 x 64 f32 tile moved 16 KiB and measured 84% of a D2D copy)
+template<typename T>
+constexpr int kTransposeSub =
+  32768 / (kTransposeTile<T> * kTransposeTile<T> * int(sizeof(T))) > 1
+    ? 32768 / (kTransposeTile<T> * kTransposeTile<T> * int(sizeof(T)))
+    : 1;
+
 template<typename T, bool VEC>
 __global__ __launch_bounds__(256) void
 transpose_kernel(const T* __restrict__ src, uint32_t rows, uint32_t cols, T* __restrict__ dst)
 {
     constexpr int TD = kTransposeTile<T>;
     constexpr int P = kTransposePitch<T>;
-    __shared__ T tile[TD * P];
-    const uint32_t c0 = blockIdx.x * TD; // source columns = destination rows
-    const uint32_t r0 = blockIdx.y * TD; // source rows = destination columns
+    constexpr int S = kTransposeSub<T>;
+    __shared__ T tile[S][TD * P];
+    const uint32_t c0 = blockIdx.x * TD;     // source columns = destination rows
+    const uint32_t rb = blockIdx.y * TD * S; // source rows = destination columns
     const int tid = threadIdx.x;
-    const bool interior = VEC && r0 + TD <= rows && c0 + TD <= cols;
+    const bool interior = VEC && rb + TD * S <= rows && c0 + TD <= cols;
     if (interior) {
         constexpr int V = 16 / int(sizeof(T));
         constexpr int VPR = TD / V;       // vectors per tile row
         constexpr int RPP = 256 / VPR;    // tile rows per pass
         const int v = tid % VPR;
+        if constexpr (S > 1) {
+            // every sub-tile's loads before the first LDS store (f32 84% ->
+            // 91% of a D2D copy, u8 likewise; the lone u16 tile measured
+            // faster with each load followed by its LDS store, below)
+            u32x4 x[S][TD / RPP];
 #pragma unroll
-        for (int r = tid / VPR; r < TD; r += RPP) {
-            const auto* p = reinterpret_cast<const u32x4*>(src + uint64_t(r0 + r) * cols + c0) + v;
-            const u32x4 x = __builtin_nontemporal_load(p);
-            T e[V];
-            __builtin_memcpy(e, &x, 16);
+            for (int t = 0; t < S; ++t) {
 #pragma unroll
-            for (int k = 0; k < V; ++k)
-                tile[r * P + v * V + k] = e[k];
+                for (int i = 0; i < TD / RPP; ++i) {
+                    const int r = tid / VPR + i * RPP;
+                    x[t][i] = __builtin_nontemporal_load(
+                      reinterpret_cast<const u32x4*>(src + uint64_t(rb + t * TD + r) * cols + c0) +
+                      v);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < S; ++t) {
+#pragma unroll
+                for (int i = 0; i < TD / RPP; ++i) {
+                    const int r = tid / VPR + i * RPP;
+                    T e[V];
+                    __builtin_memcpy(e, &x[t][i], 16);
+#pragma unroll
+                    for (int k = 0; k < V; ++k)
+                        tile[t][r * P + v * V + k] = e[k];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = tid / VPR; r < TD; r += RPP) {
+                const u32x4 x = __builtin_nontemporal_load(
+                  reinterpret_cast<const u32x4*>(src + uint64_t(rb + r) * cols + c0) + v);
+                T e[V];
+                __builtin_memcpy(e, &x, 16);
+#pragma unroll
+                for (int k = 0; k < V; ++k)
+                    tile[0][r * P + v * V + k] = e[k];
+            }
         }
         __syncthreads();
 #pragma unroll
-        for (int c = tid / VPR; c < TD; c += RPP) {
-            T e[V];
+        for (int t = 0; t < S; ++t) {
 #pragma unroll
-            for (int k = 0; k < V; ++k)
-                e[k] = tile[(v * V + k) * P + c];
-            u32x4 x;
-            __builtin_memcpy(&x, e, 16);
-            auto* q = reinterpret_cast<u32x4*>(dst + uint64_t(c0 + c) * rows + r0) + v;
-            __builtin_nontemporal_store(x, q);
+            for (int c = tid / VPR; c < TD; c += RPP) {
+                T e[V];
+#pragma unroll
+                for (int k = 0; k < V; ++k)
+                    e[k] = tile[t][(v * V + k) * P + c];
+                u32x4 y;
+                __builtin_memcpy(&y, e, 16);
+                auto* q =
+                  reinterpret_cast<u32x4*>(dst + uint64_t(c0 + c) * rows + rb + t * TD) + v;
+                __builtin_nontemporal_store(y, q);
+            }
         }
     } else {
         // one element per access; lanes sweep rows so accesses stay contiguous
         const int x = tid % TD;
-        for (int r = tid / TD; r < TD; r += 256 / TD) {
-            if (r0 + r < rows && c0 + x < cols)
-                tile[r * P + x] = src[uint64_t(r0 + r) * cols + c0 + x];
+        for (int t = 0; t < S; ++t) {
+            const uint32_t r0 = rb + t * TD;
+            for (int r = tid / TD; r < TD; r += 256 / TD) {
+                if (r0 + r < rows && c0 + x < cols)
+                    tile[t][r * P + x] = src[uint64_t(r0 + r) * cols + c0 + x];
+            }
         }
         __syncthreads();
-        for (int c = tid / TD; c < TD; c += 256 / TD) {
-            if (c0 + c < cols && r0 + x < rows)
-                dst[uint64_t(c0 + c) * rows + r0 + x] = tile[x * P + c];
+        for (int t = 0; t < S; ++t) {
+            const uint32_t r0 = rb + t * TD;
+            for (int c = tid / TD; c < TD; c += 256 / TD) {
+                if (c0 + c < cols && r0 + x < rows)
+                    dst[uint64_t(c0 + c) * rows + r0 + x] = tile[t][x * P + c];
+            }
         }
     }
 }
@@ -1561,8 +1610,9 @@ AQZ_SHARDED(launch_transpose)(int dtype,
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);
         constexpr uint32_t TD = kTransposeTile<T>;
+        constexpr uint32_t TR = TD * kTransposeSub<T>; // source rows per block
         const uint32_t bx = (cols + TD - 1) / TD;
-        const uint32_t by = (rows + TD - 1) / TD;
+        const uint32_t by = (rows + TR - 1) / TR;
         if (by > 65535)
             return hipErrorInvalidValue;
         // 16-B vectors need 16-B aligned bases and row pitches on both sides

@@ -636,7 +636,7 @@ def test_add_frame_async_errors(aqz):
 # ---- §8(f) row 2: transposed storage order and level-0 take -----------------
 
 TRANSPOSE_SHAPES = [(64, 64), (4096, 4096), (1000, 777), (129, 4100), (1, 5), (5, 1),
-                    (512, 256), (3, 200)]
+                    (512, 256), (3, 200), (192, 256), (96, 640), (384, 512)]
 
 
 @pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
