@@ -9,7 +9,8 @@
 //    writes bit row j*8+b = bit b of byte j of every element, LSB first.
 //    Both are pure permutations: HBM-bound, nbytes read + nbytes written.
 //  * crc32c: the Castagnoli CRC of a shard index table (shard.cpp:145-166),
-//    batched over many buffers, one workgroup per buffer.
+//    batched over many buffers: 16 KiB of a buffer per workgroup, or several
+//    small buffers packed into one workgroup.
 //
 // Restated from the published algorithms (c-blosc 1.21 shuffle-generic.c /
 // bitshuffle-generic.c; RFC 3720 CRC-32C); the CPU restatement the tests

@@ -22,6 +22,10 @@ FILTER_CASES = [
     (2, 4104, 4104 * 2, 1),         # 2052 elements: not a multiple of 8 groups
     (2, 200, 13, 5),                # block of 13 bytes: odd tail byte
     (4, 2, 10, 1),                  # blocksize < typesize
+    # bit shuffle rows staged through LDS (a workgroup inside one block)
+    (4, 65536, 65536 * 2 + 1024, 2),  # f32 chunk blocks + an unstaged leftover
+    (8, 65536, 65536 * 2, 2),       # f64: 2-B rows per thread
+    (2, 32768, 32768 * 3, 2),       # exactly 256 threads per block
 ]
 
 
