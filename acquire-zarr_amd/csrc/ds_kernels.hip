@@ -954,7 +954,7 @@ tile_kernel_vec(const u32x4* __restrict__ src,
     const uint32_t col_v0 = tx * tile_vecs;
     bool any = false;
     // U vectors per lane per round, all loads issued before the stores
-    constexpr uint32_t U = 4;
+    constexpr uint32_t U = 8;
     for (uint32_t e0 = threadIdx.x; e0 < n; e0 += U * blockDim.x) {
         u32x4 v[U];
 #pragma unroll
