@@ -119,6 +119,23 @@ def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
         q.wait()
 
 
+def algorithmic_bytes(geo, counts, frames: int, method: str, bpp: int):
+    """(read, read + written) algorithmic bytes of one batch step (SURVEY
+    §8(d)): every input frame read once, every emitted level frame
+    (counts[L] of level L) written once.  Decimate keeps the top-left pixel
+    and the earlier plane, so only the even rows (and, where level 1 halves
+    Z, the even planes) are needed; whole rows, because the sampled columns
+    share 64-B bursts with the skipped ones.  Every other method reads all."""
+    W, H, planes0 = geo[0]
+    read = frames * W * H * bpp
+    if method == "decimate" and len(geo) > 1:
+        rows = (H + 1) // 2 if geo[1][0] < W or geo[1][1] < H else H
+        planes = (frames + 1) // 2 if geo[1][2] < planes0 else frames
+        read = planes * rows * W * bpp
+    written = sum(counts[L] * geo[L][0] * geo[L][1] * bpp for L in range(1, len(geo)))
+    return read, read + written
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -281,19 +298,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
 
-    # algorithmic bytes per step: read every input frame once, write every
-    # emitted level frame once (counts from the batch call)
-    # Decimate samples the top-left pixel (and the earlier plane): only the
-    # even rows (and, where level 1 halves Z, the even planes) of the input
-    # are algorithmically needed.  Whole rows, because the sampled columns
-    # share 64-B bursts with the skipped ones.  Every other method reads all.
-    read_bytes = B * frame_bytes
-    if args.method == "decimate" and n_levels > 1:
-        rows = (H + 1) // 2 if geo[1][0] < W or geo[1][1] < H else H
-        planes = (B + 1) // 2 if Z and geo[1][2] < geo[0][2] else B
-        read_bytes = planes * rows * W * bpp
-    alg_bytes = read_bytes + sum(counts[L] * geo[L][0] * geo[L][1] * bpp
-                                 for L in range(1, n_levels))
+    read_bytes, alg_bytes = algorithmic_bytes(geo, counts, B, args.method, bpp)
     kind = ds.last_batch_kind()  # 1 fused 2-D cascade, 2 fused volume, 0 per-frame
     per = {1: 4, 2: 2}.get(kind)  # levels per launch (kind 3: mixed, not derived)
     launches = -(-(n_levels - 1) // per) if per else None

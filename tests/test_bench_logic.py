@@ -1,0 +1,51 @@
+"""CPU: bench.py's algorithmic-byte accounting against the
+figures the GPU runs reported (profiles/r01/methods/, whose PMC traffic
+matched them within 0.1%)."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+HEADLINE = [(4096, 4096, 1), (2048, 2048, 1), (1024, 1024, 1), (512, 512, 1), (256, 256, 1)]
+VOLUME = [(1024, 1024, 256), (512, 512, 128), (256, 256, 64)]
+
+
+@pytest.mark.parametrize("method,read,total", [
+    ("mean", 2147483648, 2860515328),
+    ("min", 2147483648, 2860515328),
+    ("decimate", 1073741824, 1786773504),   # even rows only
+])
+def test_headline_bytes(method, read, total):
+    counts = [0, 64, 64, 64, 64]
+    assert bench.algorithmic_bytes(HEADLINE, counts, 64, method, 2) == (read, total)
+    # 44,695,552 B per Mean frame
+    if method == "mean":
+        assert total // 64 == 44695552
+
+
+@pytest.mark.parametrize("method,read,total", [
+    ("mean", 536870912, 612368384),
+    ("decimate", 134217728, 209715200),     # even planes, even rows
+])
+def test_volume_bytes(method, read, total):
+    counts = [0, 128, 64]
+    assert bench.algorithmic_bytes(VOLUME, counts, 256, method, 2) == (read, total)
+
+
+def test_decimate_z_only_level_reads_every_row():
+    # level 1 halves Z only: Decimate needs every row of the even planes
+    geo = [(64, 48, 8), (64, 48, 4)]
+    read, total = bench.algorithmic_bytes(geo, [0, 4], 8, "decimate", 1)
+    assert read == 4 * 48 * 64
+    assert total == read + 4 * 48 * 64
+
+
+def test_odd_height_decimate_rows():
+    geo = [(10, 7, 1), (5, 4, 1)]
+    read, _ = bench.algorithmic_bytes(geo, [0, 3], 3, "decimate", 4)
+    assert read == 3 * 4 * 10 * 4
