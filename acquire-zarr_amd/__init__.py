@@ -302,9 +302,14 @@ class Downsampler:
         frame = np.ascontiguousarray(frame)
         if frame.dtype != self.dtype:
             raise TypeError(f"frame dtype {frame.dtype} != {self.dtype}")
-        self._pending = frame
-        self._check(lib().aqz_ds_add_frame_async(self._h, frame.ctypes.data,
-                                                 frame.nbytes))
+        # The C call first settles the previous job, whose upload may still be
+        # reading the previous frame: keep that frame alive until it returns.
+        prev, self._pending = self._pending, frame
+        try:
+            self._check(lib().aqz_ds_add_frame_async(self._h, frame.ctypes.data,
+                                                     frame.nbytes))
+        finally:
+            del prev
 
     def wait(self):
         try:

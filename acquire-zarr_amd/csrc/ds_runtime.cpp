@@ -113,6 +113,8 @@ struct aqz_ds
     std::vector<int> cached;                   // slot holding the untaken frame, -1 none
     std::vector<void*> d_partial;              // stored earlier plane (Z levels)
     hipEvent_t h2d_done = nullptr;
+    // orders a caller's stream against `stream` around a batch run on it
+    hipEvent_t join = nullptr;
     // optional pinned staging of host frames ($AQZ_PINNED_STAGING=1)
     bool staged = false;
     void* h_stage = nullptr;
@@ -630,6 +632,8 @@ release(aqz_ds* ds)
     (void)hipFree(ds->d_tin);
     if (ds->h2d_done)
         (void)hipEventDestroy(ds->h2d_done);
+    if (ds->join)
+        (void)hipEventDestroy(ds->join);
     for (int b = 0; b < 2; ++b) {
         (void)hipFree(ds->pipe.d_in[b]);
         for (void* p : ds->pipe.d_out[b])
@@ -822,6 +826,8 @@ aqz_ds_create(const aqz_level_desc* levels,
         if ((e = hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking)) != hipSuccess)
             return fail(e, "hipStreamCreate");
         if ((e = hipEventCreateWithFlags(&ds->h2d_done, hipEventDisableTiming)) != hipSuccess)
+            return fail(e, "hipEventCreate");
+        if ((e = hipEventCreateWithFlags(&ds->join, hipEventDisableTiming)) != hipSuccess)
             return fail(e, "hipEventCreate");
         if ((e = hipMalloc(&ds->d_in, ds->bytes[0])) != hipSuccess)
             return fail(e, "hipMalloc level 0");
@@ -1282,10 +1288,38 @@ aqz_ds_run_device_batch(aqz_ds* ds,
                                     std::to_string(l));
         if (int rc = bind_device(ds))
             return rc;
-        hipStream_t user = static_cast<hipStream_t>(hip_stream);
-        hipStream_t saved = ds->stream;
-        if (user)
-            ds->stream = user;
+        // A batch on the caller's stream continues the handle's own stream
+        // order: the per-frame fallback reads and writes state (the stored Z
+        // plane, level slots) that earlier add_frame calls left queued on
+        // ds->stream, and later add_frame calls must see what the batch wrote.
+        // The guard joins the two streams both ways and restores ds->stream on
+        // every exit, exceptions included.
+        struct StreamSwap
+        {
+            aqz_ds* ds;
+            hipStream_t saved, user;
+            hipError_t enter()
+            {
+                if (!user || user == saved)
+                    return hipSuccess;
+                hipError_t e = hipEventRecord(ds->join, saved);
+                if (e == hipSuccess)
+                    e = hipStreamWaitEvent(user, ds->join, 0);
+                if (e == hipSuccess)
+                    ds->stream = user;
+                return e;
+            }
+            ~StreamSwap()
+            {
+                if (ds->stream != saved) {
+                    if (hipEventRecord(ds->join, ds->stream) == hipSuccess)
+                        (void)hipStreamWaitEvent(saved, ds->join, 0);
+                    ds->stream = saved;
+                }
+            }
+        } swap{ ds, ds->stream, static_cast<hipStream_t>(hip_stream) };
+        if (hipError_t e = swap.enter(); e != hipSuccess)
+            return ds->fail(e, "run_device_batch: stream join");
 
         std::vector<uint32_t> emitted(ds->n, 0);
         int rc = AQZ_OK;
@@ -1380,9 +1414,13 @@ aqz_ds_run_device_batch(aqz_ds* ds,
                 if (volume)
                     planes >>= run.k;
             }
-            for (uint32_t l = 0; l < ds->n; ++l) {
-                emitted[l] = volume ? (n_frames >> l) : n_frames;
-                ds->count[l] += emitted[l];
+            // a failed launch leaves the counts (and the odd-stack state they
+            // carry) where they were
+            if (rc == AQZ_OK) {
+                for (uint32_t l = 0; l < ds->n; ++l) {
+                    emitted[l] = volume ? (n_frames >> l) : n_frames;
+                    ds->count[l] += emitted[l];
+                }
             }
             ds->last_batch_kind = volume ? 2 : (all_fused ? 1 : 3);
         } else {
@@ -1398,7 +1436,6 @@ aqz_ds_run_device_batch(aqz_ds* ds,
         }
         if (out_counts)
             std::copy(emitted.begin(), emitted.end(), out_counts);
-        ds->stream = saved;
         return rc;
     } catch (...) {
         return ABI_GUARD_FAIL(ds);

@@ -136,9 +136,44 @@ def algorithmic_bytes(geo, counts, frames: int, method: str, bpp: int):
     return read, read + written
 
 
-def parse():
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv, gpus: int, port: int):
+    """`python -m torch.distributed.run` starting `gpus` ranks of this script
+    with the same arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+            f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def resolve_world(args, env):
+    """('launch', N) when this process must start N ranks itself, ('run', N)
+    when it is one of N ranks (or the only one); raises SystemExit when
+    --gpus contradicts the launcher's WORLD_SIZE."""
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        n = args.gpus or 1
+        return ("launch", n) if n > 1 else ("run", 1)
+    world = int(world)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started "
+                         f"WORLD_SIZE={world} ranks")
+    return ("run", world)
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (ranks) of one node; N > 1 without a launcher "
+                        "starts N ranks via torch.distributed.run (default: "
+                        "WORLD_SIZE, else 1)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="4096x4096_u16", choices=sorted(WORKLOADS))
@@ -162,12 +197,19 @@ def parse():
                         "the ranks' frames over xGMI with RCCL p2p and gathers "
                         "the levels back; timed end to end")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    mode, world = resolve_world(args, os.environ)
+    if mode == "launch":
+        # Before torch, the library or any GPU call: the ranks run as a child
+        # process (never exec from a process that may touch the GPU); rank 0's
+        # JSON line reaches stdout through the inherited descriptors.
+        import subprocess
+        rc = subprocess.run(launcher_cmd(sys.argv[1:], world, free_port())).returncode
+        sys.exit(rc)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -294,6 +336,13 @@ def main():
     launch_ms = [a.elapsed_time(b) for a, b in evs]
     dev = "cuda" if (dist is not None and dist.get_backend() == "nccl") else "cpu"
     elapsed = max_over_ranks(elapsed, dist, dev)
+    # every rank's average launch (us), gathered for the N > 1 line
+    rank_launch_us = [float(np.mean(launch_ms)) * 1e3]
+    if dist is not None:
+        t = torch.zeros(world, dtype=torch.float64, device=dev)
+        t[rank] = rank_launch_us[0]
+        dist.all_reduce(t)
+        rank_launch_us = [float(x) for x in t.cpu()]
 
     ms_per_step = elapsed / args.steps * 1e3
     value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
@@ -310,6 +359,11 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
                 "min_launch_us": round(min(launch_ms) * 1e3, 2)}
+
+    if world > 1:
+        roofline["per_rank"] = [{"rank": r, "avg_launch_us": round(u, 2),
+                                 "frac": round(alg_bytes / (u * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+                                for r, u in enumerate(rank_launch_us)]
 
     ceiling = measure_ceiling(torch, stream, d_in, read_bytes, alg_bytes - read_bytes,
                               max(5, args.steps // 2))
@@ -382,7 +436,10 @@ def main():
                                       3: "batched, partly single-level"}.get(kind, "?"),
                        "parallelism": (f"rank-0 batch scattered/gathered over xGMI "
                                        f"(RCCL p2p) x{world}" if xgmi else
-                                       f"frame-sharded x{world}, no collective"),
+                                       f"frame-sharded x{world}, no collective")
+                                      + (f"; process group {dist.get_backend()} "
+                                         f"world_size={dist.get_world_size()}"
+                                         if dist is not None else ""),
                        "check": check},
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
@@ -594,6 +651,26 @@ def measure_traffic(args, kernel):
             "correction": "FETCH_SIZE x1024 x2 (gfx950 half-count), WRITE_SIZE x1024"}
 
 
+def host_info():
+    """CPU model and core counts of the host the CPU baseline runs on
+    (BASELINE.md §4.2): `nproc` is what this process may run on (the box's
+    CPU share is smaller than the machine; `os_cpu_count` is the machine)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nproc = os.cpu_count()
+    return {"cpu_model": model, "nproc": nproc, "os_cpu_count": os.cpu_count()}
+
+
 def measure_cpu(geo, dtype, method, seconds, frames):
     """The oracle (single-thread C port of the reference Downsampler) on a
     bounded sample of the same workload: add_frame + take_frame of every
@@ -620,7 +697,7 @@ def measure_cpu(geo, dtype, method, seconds, frames):
         if el >= seconds and n >= 4:
             break
     return {"value": round(n * W * H / el / 1e9, 4), "unit": "GPixels/s", "cores": 1,
-            "kind": "port",
+            "kind": "port", **host_info(),
             "sample": f"{n} frames of {W}x{H} {np.dtype(dtype).name} through the "
                       f"{n_levels}-level pyramid ({el:.1f} s): oracle/ds_oracle.c "
                       f"Downsampler add_frame+take_frame, single thread (-O3 -mavx2)",

@@ -133,7 +133,10 @@ typedef struct aqz_ds aqz_ds;
  * so the multiscale arrays of one process spread over a node's GPUs (their
  * frames are independent: no collective).  An ordinal that names no visible
  * device is AQZ_INVALID_ARGUMENT.
- * Allocates all device buffers and pinned staging up front.
+ * Allocates the level-0 frame, two slots per level and the stored Z planes
+ * on the device up front; pinned memory only for the eager readback of small
+ * pyramids and for $AQZ_PINNED_STAGING=1.  Tile scratch, the host-batch
+ * pipeline and the upload thread are allocated on first use.
  */
 int aqz_ds_create(const aqz_level_desc* levels,
                   uint32_t n_levels,
@@ -150,8 +153,10 @@ void aqz_ds_destroy(aqz_ds* ds);
  * `Downsampler::add_frame` (downsampler.cpp:306-401): same level cascade, Z
  * pairing, odd-plane pass-through and emit/no-overwrite rules.
  * `nbytes` must equal width*height*bytes_of_type at level 0.
- * The host buffer is read only during the call (it is staged to pinned
- * memory before return), so the caller may reuse it immediately.
+ * The host buffer is read only during the call: it is uploaded straight from
+ * the caller's (pageable) memory and the call returns once that upload has
+ * completed ($AQZ_PINNED_STAGING=1: staged through a pinned buffer instead),
+ * so the caller may reuse it immediately.
  * Kernels and device->host copies are queued asynchronously; the level
  * frames are synchronised in aqz_ds_take_frame.
  */

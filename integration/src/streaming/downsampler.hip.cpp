@@ -1,0 +1,209 @@
+// downsampler.hip.cpp — zarr::Downsampler on MI355X (acquire-zarr v0.8.1).
+//
+// Goes into the reference tree as src/streaming/downsampler.hip.cpp and is
+// compiled only when AQZ_DOWNSAMPLER=hip (cmake/hip.cmake, which also defines
+// AQZ_DOWNSAMPLER_HIP and links libaqz_downsampler).  It defines the
+// per-frame half of the class over the C ABI in include/aqz_downsampler.h:
+//
+//   Downsampler(config, method)  downsampler.cpp:249-304  -> aqz_ds_create
+//   ~Downsampler()               (implicit)               -> aqz_ds_destroy
+//   add_frame(frame)             downsampler.cpp:306-401  -> aqz_ds_add_frame
+//   take_frame(level, out)       downsampler.cpp:403-414  -> aqz_ds_take_frame
+//   add_frame_async(frame)       new -> aqz_ds_add_frame_async
+//   wait()                       new                      -> aqz_ds_wait
+//   take_frame_tiled(level, t)   new -> aqz_ds_take_frame_tiled
+//   level_is_tiled(level)        new
+//
+// The rest of the class stays in the reference's downsampler.cpp, compiled
+// unchanged: acquire-zarr-hip.patch only puts the CPU constructor, add_frame,
+// take_frame, emplace_downsampled_frame_ and the scalar kernels they use
+// (downsampler.cpp:39-414, 599-605) under #ifndef AQZ_DOWNSAMPLER_HIP.  So
+// make_writer_configurations_ (the level geometry MultiscaleArray builds its
+// arrays from), writer_configurations, downsampling_method and get_metadata
+// (the OME metadata) are the reference's own code, and the level geometry
+// handed to the GPU is read back from those configurations.
+//
+// Error behaviour is the reference's: every failure throws std::runtime_error
+// (EXPECT, macros.hh), which MultiscaleArray::create_downsampler_ logs and
+// turns into a failed ZarrStream_create (multiscale.array.cpp:172-189), and
+// which the frame-queue consumer turns into a stream error
+// (zarr.stream.cpp:1705-1720).
+
+#include "downsampler.hh"
+#include "macros.hh"
+
+#include "aqz_downsampler.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace {
+
+// The reference validates the dtype before the method, with these messages
+// (downsampler.cpp:295-302).
+void
+check_dtype_and_method(ZarrDataType dtype, ZarrDownsamplingMethod method)
+{
+    if (static_cast<int>(dtype) < 0 || dtype >= ZarrDataTypeCount) {
+        throw std::runtime_error("Invalid data type: " + std::to_string(dtype));
+    }
+    EXPECT(method < ZarrDownsamplingMethodCount,
+           "Invalid downsampling method: ",
+           static_cast<int>(method));
+}
+
+} // namespace
+
+zarr::Downsampler::Downsampler(std::shared_ptr<ArrayConfig> config,
+                               ZarrDownsamplingMethod method)
+{
+    make_writer_configurations_(config); // reference code, downsampler.cpp
+    check_dtype_and_method(config->dtype, method);
+    method_ = method;
+
+    // Per-level geometry exactly as add_frame reads it (downsampler.cpp:
+    // 309-338): width/height are the storage-order last two dimensions,
+    // planes is dimension ndims-3 (the phantom singleton for 2-D arrays).
+    const size_t n = n_levels_();
+    std::vector<aqz_level_desc> levels(n);
+    for (size_t level = 0; level < n; ++level) {
+        const auto& dims = writer_configurations_.at(int(level))->dimensions;
+        levels[level].width = dims->width_dim().array_size_px;
+        levels[level].height = dims->height_dim().array_size_px;
+        levels[level].planes = dims->at(dims->ndims() - 3).array_size_px;
+    }
+
+    aqz_ds* handle = nullptr;
+    const int rc = aqz_ds_create(levels.data(),
+                                 static_cast<uint32_t>(n),
+                                 static_cast<int>(config->dtype),
+                                 static_cast<int>(method),
+                                 -1, // $AQZ_GPU_DEVICE, else the current device
+                                 &handle);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_last_error());
+    gpu_ = handle;
+
+    // Levels >= 1 are tiled on the GPU right behind the pyramid, in their
+    // own chunk shape (downsample_dimension keeps chunk sizes), so that
+    // MultiscaleArray can hand each tile to its chunk in one copy
+    // (array.tiled.cpp).  A transposed storage order keeps the row-major
+    // path: Array chunks the transpose of what it is given.
+    tiles_.assign(n, { 0u, 0u });
+    if (config->dimensions->needs_xy_transposition()) {
+        return;
+    }
+    for (size_t level = 1; level < n; ++level) {
+        const auto& dims = writer_configurations_.at(int(level))->dimensions;
+        const uint32_t tile_rows = dims->height_dim().chunk_size_px;
+        const uint32_t tile_cols = dims->width_dim().chunk_size_px;
+        if (tile_rows == 0 || tile_cols == 0) {
+            continue;
+        }
+        EXPECT(aqz_ds_set_level_tiling(
+                 gpu_, uint32_t(level), tile_rows, tile_cols) == AQZ_OK,
+               "GPU downsampler: ",
+               aqz_ds_last_error(gpu_));
+        tiles_[level] = { tile_rows, tile_cols };
+    }
+}
+
+zarr::Downsampler::~Downsampler()
+{
+    aqz_ds_destroy(gpu_); // settles a pending add_frame_async first
+}
+
+void
+zarr::Downsampler::add_frame(std::vector<uint8_t>& frame)
+{
+    const int rc = aqz_ds_add_frame(gpu_, frame.data(), frame.size());
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+}
+
+void
+zarr::Downsampler::add_frame_async(std::vector<uint8_t>& frame)
+{
+    const int rc = aqz_ds_add_frame_async(gpu_, frame.data(), frame.size());
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+}
+
+void
+zarr::Downsampler::wait()
+{
+    const int rc = aqz_ds_wait(gpu_);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+}
+
+bool
+zarr::Downsampler::take_frame(int level, std::vector<uint8_t>& frame_data)
+{
+    // The reference returns false for any level it holds no frame for,
+    // including out-of-range ones (downsampler.cpp:403-414).
+    if (level < 1 || static_cast<size_t>(level) >= n_levels_()) {
+        return false;
+    }
+    // Size query first: the frame stays cached until it is copied out.
+    size_t nbytes = 0;
+    int has_frame = 0;
+    int rc = aqz_ds_take_frame(
+      gpu_, static_cast<uint32_t>(level), nullptr, 0, &nbytes, &has_frame);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+    if (!has_frame) {
+        return false;
+    }
+    // The reference hands its cached vector over by swap, so the caller's
+    // buffer ends up exactly the level frame's size.
+    frame_data.resize(nbytes);
+    rc = aqz_ds_take_frame(gpu_,
+                           static_cast<uint32_t>(level),
+                           frame_data.data(),
+                           frame_data.size(),
+                           &nbytes,
+                           &has_frame);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+    return has_frame != 0;
+}
+
+bool
+zarr::Downsampler::level_is_tiled(int level) const
+{
+    return level >= 1 && static_cast<size_t>(level) < tiles_.size() &&
+           tiles_[level].first != 0;
+}
+
+bool
+zarr::Downsampler::take_frame_tiled(int level, std::vector<uint8_t>& tiles)
+{
+    if (!level_is_tiled(level)) {
+        return false;
+    }
+    const auto [tile_rows, tile_cols] = tiles_[level];
+    size_t nbytes = 0;
+    int has_frame = 0;
+    int rc = aqz_ds_take_frame_tiled(gpu_,
+                                     static_cast<uint32_t>(level),
+                                     tile_rows,
+                                     tile_cols,
+                                     nullptr,
+                                     0,
+                                     nullptr,
+                                     &nbytes,
+                                     &has_frame);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+    if (!has_frame) {
+        return false;
+    }
+    // The chunk zero scan stays with Chunk::write_tile_rows, which stops at
+    // the first nonzero byte; the tiles alone travel.
+    tiles.resize(nbytes);
+    rc = aqz_ds_take_frame_tiled(gpu_,
+                                 static_cast<uint32_t>(level),
+                                 tile_rows,
+                                 tile_cols,
+                                 tiles.data(),
+                                 tiles.size(),
+                                 nullptr,
+                                 &nbytes,
+                                 &has_frame);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+    return has_frame != 0;
+}

@@ -49,3 +49,30 @@ def test_odd_height_decimate_rows():
     geo = [(10, 7, 1), (5, 4, 1)]
     read, _ = bench.algorithmic_bytes(geo, [0, 3], 3, "decimate", 4)
     assert read == 3 * 4 * 10 * 4
+
+
+# ---- --gpus N: the launcher ------------------------------
+
+def test_gpus_without_launcher_starts_n_ranks():
+    args = bench.parse(["--gpus", "8", "--steps", "3"])
+    assert bench.resolve_world(args, {}) == ("launch", 8)
+    cmd = bench.launcher_cmd(["--gpus", "8", "--steps", "3"], 8, 29555)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    i = cmd.index(os.path.abspath(bench.__file__))
+    assert cmd[i + 1:] == ["--gpus", "8", "--steps", "3"]  # same arguments
+
+
+def test_single_gpu_runs_in_process():
+    assert bench.resolve_world(bench.parse([]), {}) == ("run", 1)
+    assert bench.resolve_world(bench.parse(["--gpus", "1"]), {}) == ("run", 1)
+
+
+def test_under_launcher_world_size_wins():
+    # the driver: torch.distributed.run --nproc-per-node N bench.py --gpus N
+    env = {"WORLD_SIZE": "4", "RANK": "2"}
+    assert bench.resolve_world(bench.parse(["--gpus", "4"]), env) == ("run", 4)
+    assert bench.resolve_world(bench.parse([]), env) == ("run", 4)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(bench.parse(["--gpus", "8"]), env)

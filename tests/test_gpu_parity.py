@@ -623,6 +623,80 @@ def test_add_frame_async_matches_oracle(aqz, oracle, geo_kind):
     ds.close()
 
 
+def test_add_frame_async_temporaries(aqz, oracle):
+    """Frames passed as temporaries: the binding must keep each one alive
+    until the next call has settled its upload.  Each temporary
+    is dropped right after the call and new arrays of the same size are
+    allocated and scribbled over, so a freed buffer would be reused."""
+    geo = halving_geometry(2048, 1024, 4)
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+    rng = np.random.default_rng(seed_of("async-temp"))
+    base = rng.integers(0, 65536, (6, 1024, 2048), dtype=np.uint16)
+    for i in range(6):
+        ds.add_frame_async(np.ascontiguousarray(base[i][:, ::1].copy()))
+        junk = [np.full((1024, 2048), 0xA5A5, np.uint16) for _ in range(3)]
+        del junk
+        ref.add_frame(base[i])
+        if i % 3 == 2:  # two back-to-back temporaries, then takes
+            continue
+        for L in range(1, len(geo)):
+            a, b = ds.take_frame(L), ref.take_frame(L)
+            assert (a is None) == (b is None), f"frame {i} L{L} readiness"
+            if a is not None:
+                assert_parity(a, b, f"temporary frame {i} L{L}")
+    ds.wait()
+    ds.close()
+
+
+def test_stream_batch_stream_interleave(aqz, oracle):
+    """add_frame, then run_device_batch on a caller stream, then add_frame
+    again on a Z-halving pyramid: the batch's per-frame fallback consumes the
+    earlier plane the first add_frame stored on the handle's stream, and the
+    later add_frame consumes the plane the batch stored (the two
+    streams are joined both ways)."""
+    torch = torch_cuda()
+    geo = [(2048, 1024, 8), (1024, 512, 4), (512, 256, 2)]
+    rng = np.random.default_rng(seed_of("interleave"))
+    frames = rng.integers(0, 65536, (8, 1024, 2048), dtype=np.uint16)
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+
+    def stream_one(i):
+        ds.add_frame(frames[i])
+        ref.add_frame(frames[i])
+        for L in range(1, len(geo)):
+            a, b = ds.take_frame(L), ref.take_frame(L)
+            assert (a is None) == (b is None), f"frame {i} L{L} readiness"
+            if a is not None:
+                assert_parity(a, b, f"streamed frame {i} L{L}")
+
+    stream_one(0)  # stores the earlier plane of level 1
+    nb = 4  # frames 1..4: frame 4 is stored as the next earlier plane
+    d_in = to_device(frames[1:1 + nb])
+    outs = [None] + [empty_device(nb * w * h * 2) for w, h, _ in geo[1:]]
+    counts = ds.run_device_batch(d_in.data_ptr(), nb, [0] + [o.data_ptr() for o in outs[1:]],
+                                 launch_stream())
+    assert ds.last_batch_kind() == 0  # a stored plane forces the per-frame path
+    want = {L: [] for L in range(1, len(geo))}
+    for i in range(1, 1 + nb):
+        ref.add_frame(frames[i])
+        for L in want:
+            r = ref.take_frame(L)
+            if r is not None:
+                want[L].append(r)
+    for L in want:
+        w, h, _ = geo[L]
+        assert counts[L] == len(want[L]), f"L{L} count"
+        got = from_device(outs[L], np.uint16, (nb, h, w))
+        for k, r in enumerate(want[L]):
+            assert_parity(got[k], r, f"batch L{L} #{k}")
+    torch.cuda.synchronize()
+    for i in range(1 + nb, 8):  # frame 5 pairs with the plane the batch stored
+        stream_one(i)
+    ds.close()
+
+
 def test_add_frame_async_errors(aqz):
     geo = halving_geometry(64, 64, 2)
     ds = aqz.Downsampler(geo, np.uint16, 1)
