@@ -34,6 +34,7 @@ EXPORTS = (
     "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
     "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
+    "aqz_ds_run_device_batch_tiled", "aqz_ds_tiled_flag_slots",
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
     "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_set_input_transpose",
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
@@ -103,6 +104,11 @@ def lib() -> ctypes.CDLL:
                                     ctypes.POINTER(i32)]
     L.aqz_ds_run_device_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp),
                                           ctypes.POINTER(u32), vp]
+    L.aqz_ds_run_device_batch_tiled.argtypes = [vp, vp, u32, ctypes.POINTER(u32),
+                                                ctypes.POINTER(u32), ctypes.POINTER(vp),
+                                                ctypes.POINTER(vp), ctypes.POINTER(u32), vp]
+    L.aqz_ds_tiled_flag_slots.argtypes = [vp, u32, u32, u32]
+    L.aqz_ds_tiled_flag_slots.restype = u32
     L.aqz_ds_take_frame_tiled.argtypes = [vp, u32, u32, u32, vp, sz, vp,
                                           ctypes.POINTER(sz), ctypes.POINTER(i32)]
     L.aqz_ds_set_level_tiling.argtypes = [vp, u32, u32, u32]
@@ -280,7 +286,8 @@ class Downsampler:
 
     def last_batch_kind(self) -> int:
         """0 per-frame, 1 fused 2-D cascade, 2 fused volume, 3 2-D batch with
-        some runs on batched single-level kernels, -1 none."""
+        some runs on batched single-level kernels, 4 fused 2-D cascade writing
+        chunk tiles, -1 none."""
         return lib().aqz_ds_last_batch_kind(self._h)
 
     def device_memory_usage(self) -> int:
@@ -330,6 +337,30 @@ class Downsampler:
                                             out.nbytes, ctypes.byref(nb),
                                             ctypes.byref(has)))
         return out if has.value else None
+
+    def run_device_batch_tiled(self, device_frames: int, n_frames: int, tiles,
+                               device_outs, device_nonzero=None, stream: int = 0):
+        """Device-resident batch with every level chunk-tiled by the pyramid
+        kernel: `tiles[L]` = (tile_rows, tile_cols), `device_outs[L]` /
+        `device_nonzero[L]` device pointers (index 0 ignored; nonzero
+        optional, tiled_flag_slots(L, ...) bytes per tile).  Returns frames
+        emitted per level."""
+        n = self.n_levels
+        tr = (ctypes.c_uint32 * n)(*[int(t[0]) if t else 0 for t in tiles])
+        tc = (ctypes.c_uint32 * n)(*[int(t[1]) if t else 0 for t in tiles])
+        outs = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in device_outs])
+        nz = None
+        if device_nonzero is not None:
+            nz = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in device_nonzero])
+        counts = (ctypes.c_uint32 * n)()
+        self._check(lib().aqz_ds_run_device_batch_tiled(
+            self._h, device_frames, n_frames, tr, tc, outs, nz, counts,
+            ctypes.c_void_p(stream) if stream else None))
+        return list(counts)
+
+    def tiled_flag_slots(self, level: int, tile_rows: int, tile_cols: int) -> int:
+        """Zero-scan flag bytes per tile of run_device_batch_tiled at `level`."""
+        return lib().aqz_ds_tiled_flag_slots(self._h, level, tile_rows, tile_cols)
 
     def run_device_batch(self, device_frames: int, n_frames: int, device_outs,
                          stream: int = 0):

@@ -9,8 +9,8 @@
 #ifndef AQZ_SHARDS
 #error "ds_dispatch.cpp is built with -DAQZ_SHARDS=<n> (acquire-zarr_amd/Makefile)"
 #endif
-#if AQZ_SHARDS != 4
-#error "ds_dispatch.cpp routes to exactly 4 shards"
+#if AQZ_SHARDS != 8
+#error "ds_dispatch.cpp routes to exactly 8 shards"
 #endif
 
 namespace aqz {
@@ -19,7 +19,11 @@ namespace aqz {
     hipError_t name##_shard0 params;                                           \
     hipError_t name##_shard1 params;                                           \
     hipError_t name##_shard2 params;                                           \
-    hipError_t name##_shard3 params;
+    hipError_t name##_shard3 params;                                           \
+    hipError_t name##_shard4 params;                                           \
+    hipError_t name##_shard5 params;                                           \
+    hipError_t name##_shard6 params;                                           \
+    hipError_t name##_shard7 params;
 
 #define AQZ_ROUTE(name, dtype, args)                                           \
     do {                                                                       \
@@ -32,14 +36,25 @@ namespace aqz {
                 return name##_shard1 args;                                     \
             case 2:                                                            \
                 return name##_shard2 args;                                     \
-            default:                                                           \
+            case 3:                                                            \
                 return name##_shard3 args;                                     \
+            case 4:                                                            \
+                return name##_shard4 args;                                     \
+            case 5:                                                            \
+                return name##_shard5 args;                                     \
+            case 6:                                                            \
+                return name##_shard6 args;                                     \
+            default:                                                           \
+                return name##_shard7 args;                                     \
         }                                                                      \
     } while (0)
 
 AQZ_DECLARE_SHARDS(launch_cascade,
                    (int, int, const void*, uint64_t, uint32_t, uint32_t, const LevelOut*, int,
                     uint32_t, hipStream_t))
+AQZ_DECLARE_SHARDS(launch_cascade_tiled,
+                   (int, int, const void*, uint64_t, uint32_t, uint32_t, const LevelOut*,
+                    const TiledOut*, int, uint32_t, hipStream_t))
 AQZ_DECLARE_SHARDS(launch_volume,
                    (int, int, const void*, uint64_t, uint32_t, uint32_t, const LevelOut*, int,
                     uint32_t, hipStream_t))
@@ -71,6 +86,23 @@ launch_cascade(int dtype,
 {
     AQZ_ROUTE(launch_cascade, dtype,
               (dtype, method, src, src_frame_elems, W, H, outs, n_out, n_frames, stream));
+}
+
+hipError_t
+launch_cascade_tiled(int dtype,
+                     int method,
+                     const void* src,
+                     uint64_t src_frame_elems,
+                     uint32_t W,
+                     uint32_t H,
+                     const LevelOut* outs,
+                     const TiledOut* touts,
+                     int n_out,
+                     uint32_t n_frames,
+                     hipStream_t stream)
+{
+    AQZ_ROUTE(launch_cascade_tiled, dtype,
+              (dtype, method, src, src_frame_elems, W, H, outs, touts, n_out, n_frames, stream));
 }
 
 hipError_t

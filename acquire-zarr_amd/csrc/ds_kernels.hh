@@ -69,6 +69,56 @@ hipError_t launch_cascade(int dtype,
                           uint32_t n_frames,
                           hipStream_t stream);
 
+// Chunk-tiled output of one cascade level: frame k of
+// the level at ptr + k * n_tiles * tile_rows * tile_cols elements, tile
+// t = ty * n_tiles_x + tx holding tile_rows x tile_cols elements row-major,
+// zero where it overhangs the level — the layout Array::write_frame_to_chunks_
+// fills (array.cpp:507-622, chunk.cpp:17-58).  `nonzero` (optional, device)
+// receives the chunk zero scan as flag bytes (cascade_tiled_slots).
+struct TiledOut
+{
+    void* ptr;
+    uint32_t tile_rows, tile_cols;
+    uint8_t* nonzero;
+};
+
+// Columns per lane launch_cascade_tiled uses for W-wide frames of `dtype`
+// (cascade_pick_cols for element-aligned buffers).
+uint32_t cascade_tiled_cols(int dtype, uint32_t W);
+
+// Zero-scan flag bytes per tile that launch_cascade_tiled writes for level
+// `level` (1-based within a launch of n_out levels over W-wide frames): when
+// the kernel's wave blocks tile the chunk tiles exactly, `slots` bytes per
+// tile (*slots_x across), each written once by the wave owning that block —
+// the tile is nonzero iff any of its slots is; returns 0 otherwise (one byte
+// per tile, cleared before the launch).
+uint32_t cascade_tiled_slots(int dtype,
+                             uint32_t W,
+                             int n_out,
+                             int level,
+                             uint32_t tile_rows,
+                             uint32_t tile_cols,
+                             uint32_t* slots_x);
+
+// launch_cascade with every level written chunk-tiled from registers: one
+// kernel, whose trailing waves zero-fill the tile overhang past the frame
+// (plus one flag clear per level whose tiles do not hold whole wave blocks).
+// touts[i].nonzero then holds n_frames * n_tiles * max(1, slots) bytes.
+// outs[i] gives level i's geometry; its ptr, when non-null, also receives the
+// level row-major (the input of a following launch).  Same geometry rules as
+// launch_cascade.
+hipError_t launch_cascade_tiled(int dtype,
+                                int method,
+                                const void* src,
+                                uint64_t src_frame_elems,
+                                uint32_t W,
+                                uint32_t H,
+                                const LevelOut* outs,
+                                const TiledOut* touts,
+                                int n_out,
+                                uint32_t n_frames,
+                                hipStream_t stream);
+
 // Fused 2x2x2 (XY reduce, then Z pair) over `n_planes` consecutive planes for
 // pyramids whose levels all halve both XY and Z; n_planes must be a multiple
 // of 2^n_out, n_out in [1, kMaxVolumeLevels].  Level L receives

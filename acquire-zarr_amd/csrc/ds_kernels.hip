@@ -292,7 +292,44 @@ struct CascadeParams
     uint64_t dst_frame_elems[kMaxFusedLevels];
     uint32_t w[kMaxFusedLevels];
     uint32_t h[kMaxFusedLevels];
+    // Chunk-tiled outputs (cascade_kernel<..., TILED = true>, launch_cascade_tiled):
+    // level J-1's tiles at tdst + frame * tframe_elems, tile t = ty * ntx + tx,
+    // tr x tc elements row-major; the padded level is pw x ph.  dst[J-1] may
+    // then be null (no row-major copy).
+    uint8_t* tdst[kMaxFusedLevels];
+    uint64_t tframe_elems[kMaxFusedLevels];
+    uint32_t tr[kMaxFusedLevels], tc[kMaxFusedLevels], ntx[kMaxFusedLevels];
+    uint32_t pw[kMaxFusedLevels], ph[kMaxFusedLevels];
+    // Zero scan.  slots[J-1] > 0 (the wave's level-J block always lies in one
+    // tile): tile t owns `slots` flag bytes, one per wave block it holds
+    // (slots_x across), and every slot is written exactly once — by its wave,
+    // or as 0 by the zero-fill waves for blocks past the grid — so nothing is
+    // cleared first.  slots[J-1] == 0: one byte per tile, cleared before the
+    // launch, set to 1 by every wave storing a nonzero byte into the tile.
+    uint8_t* flags[kMaxFusedLevels];
+    uint32_t flags_frame[kMaxFusedLevels];
+    uint32_t slots[kMaxFusedLevels], slots_x[kMaxFusedLevels];
+    // Zero-fill waves (wave ids >= total_units): the padded area the grid's
+    // blocks do not reach — columns >= cov_w, and rows >= cov_h — per
+    // (frame, level, padded row) item, plus the slot flags of those blocks.
+    uint32_t cov_w[kMaxFusedLevels], cov_h[kMaxFusedLevels];
+    uint32_t zrows[kMaxFusedLevels]; // items of the level per frame
+    uint32_t zitems;                 // items per frame, all levels
+    uint32_t zwaves;                 // zero-fill waves: the grid's first zwaves / 4 blocks
+    uint32_t main_blocks;            // blocks of cascade waves after them
+    uint32_t remap;                  // 1: XCD-contiguous block order (cascade_kernel)
 };
+
+// $AQZ_XCD_REMAP: unset = the launcher's default, 0 = off, 1 = on (A/B only).
+inline int
+xcd_remap_env()
+{
+    static const int v = [] {
+        const char* e = std::getenv("AQZ_XCD_REMAP");
+        return (e && *e) ? std::atoi(e) : -1;
+    }();
+    return v;
+}
 
 // Columns of T per lane in the fused cascade: 16 bytes for 1- and 2-byte
 // types, 32 bytes (two 16-byte loads per row) for 4- and 8-byte types, which
@@ -405,6 +442,201 @@ store_level(T* dst,
     }
 }
 
+// Any nonzero byte (the chunk zero scan is byte-wise: -0.0 counts).
+template<typename T>
+__device__ __forceinline__ bool
+nonzero_bits(T x)
+{
+    if constexpr (sizeof(T) == 8) {
+        uint64_t b;
+        __builtin_memcpy(&b, &x, 8);
+        return b != 0;
+    } else {
+        uint32_t b = 0;
+        __builtin_memcpy(&b, &x, sizeof(T));
+        return b != 0;
+    }
+}
+
+// Write the lane's RO x CO block of level J in chunk-tile order (the layout
+// Array::write_frame_to_chunks_ fills, array.cpp:507-622): element (row, col)
+// goes to tile (row / tr, col / tc) at (row % tr) * tc + col % tc.  Positions
+// past the level inside the padded pw x ph area are stored as zero — the
+// bytes Chunk::write_tile_rows leaves in an overhanging tile slot
+// (chunk.cpp:17-58) — and positions past the padding are skipped.  `wc0` is
+// the wave's first level-0 column (uniform).  Flags: see CascadeParams.
+template<typename T, int C, int J, int RO, int CO, bool EDGE>
+__device__ __forceinline__ void
+store_level_tiled(const CascadeParams& p,
+                  const T (&out)[RO][CO],
+                  uint32_t f,
+                  uint32_t wc0,
+                  uint32_t row0,
+                  int lane)
+{
+    constexpr int SO = kLaneStride<C, J>;
+    constexpr int I = J - 1;
+    const uint32_t w = p.w[I], h = p.h[I], tr = p.tr[I], tc = p.tc[I];
+    const uint32_t pw = p.pw[I], ph = p.ph[I];
+    const uint32_t lc = (uint32_t(lane) * C) >> J; // lane's column offset in the block
+    const uint32_t bc = wc0 >> J;                    // block's first level column (uniform)
+    const uint32_t br = row0 >> J;                   // block's first level row (uniform)
+    const uint32_t cout0 = bc + lc;
+    const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
+    const uint64_t tile_elems = uint64_t(tr) * tc;
+    T* base = reinterpret_cast<T*>(p.tdst[I]) + uint64_t(f) * p.tframe_elems[I];
+    uint8_t* flags = p.flags[I] ? p.flags[I] + uint64_t(f) * p.flags_frame[I] : nullptr;
+    const uint32_t K = p.slots[I];
+    if (K) {
+        // The block lies in one tile: uniform tile coordinates, lane offsets
+        // add to the block's column inside it.
+        if (br >= ph || bc >= pw)
+            return; // past the padding (uniform): no tile, no slot
+        const uint32_t ty = br / tr, tx = bc / tc;
+        const uint32_t ry0 = br - ty * tr, cx = bc - tx * tc + lc;
+        T* tile = base + (uint64_t(ty) * p.ntx[I] + tx) * tile_elems;
+        bool nz = false;
+#pragma unroll
+        for (int r = 0; r < RO; ++r) {
+            const uint32_t row = br + r;
+            if (!leader)
+                continue;
+            T v[CO];
+#pragma unroll
+            for (int c = 0; c < CO; ++c) {
+                T x = out[r][c];
+                if constexpr (EDGE) {
+                    if (row >= h || cout0 + c >= w)
+                        x = T(0);
+                }
+                v[c] = x;
+                nz = nz || nonzero_bits(x);
+            }
+            store_vec<T, CO, true>(tile + uint64_t(ry0 + r) * tc + cx, v);
+        }
+        const bool any = __ballot(nz) != 0; // every lane reaches the vote
+        if (flags && lane == 0) {
+            // the block is RO level rows by 64*C >> J level columns
+            constexpr uint32_t BW = (64u * C) >> J;
+            const uint32_t slot = (ry0 / RO) * p.slots_x[I] + (bc - tx * tc) / BW;
+            flags[(uint64_t(ty) * p.ntx[I] + tx) * K + slot] = any ? 1 : 0;
+        }
+        return;
+    }
+    // General geometry: per-row tile coordinates, per-lane tile columns.
+    const uint32_t tx = cout0 / tc;
+    const uint32_t cx = cout0 - tx * tc;
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+        const uint32_t row = br + r;
+        bool ok = leader;
+        if constexpr (EDGE) {
+            ok = ok && row < ph && cout0 < pw;
+        }
+        if (!ok)
+            continue;
+        const uint32_t ty = row / tr;
+        T* trow = base + uint64_t(ty) * p.ntx[I] * tile_elems + uint64_t(row - ty * tr) * tc;
+        T v[CO];
+        bool rnz = false;
+#pragma unroll
+        for (int c = 0; c < CO; ++c) {
+            T x = out[r][c];
+            if constexpr (EDGE) {
+                if (row >= h || cout0 + c >= w)
+                    x = T(0);
+            }
+            v[c] = x;
+            rnz = rnz || nonzero_bits(x);
+        }
+        if (cx + CO <= tc) {
+            store_vec<T, CO, true>(trow + tx * tile_elems + cx, v);
+            if (rnz && flags)
+                flags[ty * p.ntx[I] + tx] = 1;
+        } else {
+            // the lane's columns cross a tile edge (tc not a multiple of CO)
+#pragma unroll
+            for (int c = 0; c < CO; ++c) {
+                const uint32_t col = cout0 + c;
+                if (col >= pw)
+                    continue;
+                const uint32_t ctx = col / tc;
+                const T one[1] = { v[c] };
+                store_vec<T, 1, true>(trow + ctx * tile_elems + (col - ctx * tc), one);
+                if (flags && nonzero_bits(v[c]))
+                    flags[ty * p.ntx[I] + ctx] = 1;
+            }
+        }
+    }
+}
+
+// Zero-fill wave `z` of `nz` (tiled cascade): the padded tile area past the
+// grid's blocks, item by item — item = (frame, level, padded row), covering
+// columns [cov_w, pw) of rows < cov_h and whole rows >= cov_h — then the
+// slot flags of the blocks past the grid.  16-byte stores inside each tile's
+// row segment, element stores at the segment ends.
+template<typename T>
+__device__ __forceinline__ void
+zero_fill_tiled(const CascadeParams& p, uint32_t z, uint32_t nz, int lane, int n_out,
+                uint32_t n_frames)
+{
+    constexpr int E = 16 / int(sizeof(T));
+    const uint64_t items = uint64_t(p.zitems) * n_frames;
+    for (uint64_t it = z; it < items; it += nz) {
+        const uint32_t f = uint32_t(it / p.zitems);
+        uint32_t rem = uint32_t(it - uint64_t(f) * p.zitems);
+        int I = 0;
+        while (I + 1 < n_out && rem >= p.zrows[I]) {
+            rem -= p.zrows[I];
+            ++I;
+        }
+        const uint32_t tr = p.tr[I], tc = p.tc[I], pw = p.pw[I];
+        const uint32_t cw = min(p.cov_w[I], pw), chh = min(p.cov_h[I], p.ph[I]);
+        const uint32_t row = cw < pw ? rem : chh + rem;
+        const uint32_t a = row >= chh ? 0u : cw;
+        const uint64_t tile_elems = uint64_t(tr) * tc;
+        const uint32_t ty = row / tr;
+        T* trow = reinterpret_cast<T*>(p.tdst[I]) + uint64_t(f) * p.tframe_elems[I] +
+                  uint64_t(ty) * p.ntx[I] * tile_elems + uint64_t(row - ty * tr) * tc;
+        for (uint32_t tx = a / tc; tx * tc < pw; ++tx) {
+            const uint32_t c0 = max(a, tx * tc) - tx * tc; // segment [c0, tc) in the tile row
+            T* seg = trow + tx * tile_elems + c0;
+            const uint32_t len = tc - c0;
+            for (uint32_t i = uint32_t(lane) * E; i < len; i += 64u * E) {
+                if (i + E <= len) {
+                    const T zeros[E] = {};
+                    store_vec<T, E, true>(seg + i, zeros);
+                } else {
+                    for (uint32_t k = i; k < len; ++k) {
+                        const T zero[1] = { T(0) };
+                        store_vec<T, 1, true>(seg + k, zero);
+                    }
+                }
+            }
+        }
+    }
+    // slot flags of blocks no wave of the grid owns (rows >= cov_h or
+    // columns >= cov_w at their level)
+    for (int I = 0; I < n_out; ++I) {
+        if (!p.slots[I] || !p.flags[I] || (p.cov_w[I] >= p.pw[I] && p.cov_h[I] >= p.ph[I]))
+            continue;
+        const uint32_t K = p.slots[I], kx = p.slots_x[I], ky = K / kx;
+        const uint32_t bh = p.tr[I] / ky, bw = p.tc[I] / kx; // block size at the level
+        const uint64_t per_frame = p.flags_frame[I];
+        const uint64_t total = per_frame * n_frames;
+        for (uint64_t q = uint64_t(z) * 64 + lane; q < total; q += uint64_t(nz) * 64) {
+            const uint32_t f = uint32_t(q / per_frame);
+            const uint32_t s = uint32_t(q - uint64_t(f) * per_frame);
+            const uint32_t t = s / K, slot = s - t * K;
+            const uint32_t ty = t / p.ntx[I], tx = t - ty * p.ntx[I];
+            const uint32_t r0 = ty * p.tr[I] + (slot / kx) * bh;
+            const uint32_t c0 = tx * p.tc[I] + (slot % kx) * bw;
+            if (r0 >= p.cov_h[I] || c0 >= p.cov_w[I])
+                p.flags[I][q] = 0;
+        }
+    }
+}
+
 // Row-band staging (cascade_band_kernel): levels whose rows split 64-byte
 // DRAM bursts are written to LDS first, so that one workgroup — which owns
 // a whole row band of the frame — stores each level's band as one
@@ -452,7 +684,7 @@ stage_level(const StageCtx& sc,
 
 // Level J of the 2-D cascade: reduce, store, recurse to J+1.
 template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
-         bool NTS = false, bool STAGED = false>
+         bool NTS = false, bool STAGED = false, bool TILED = false>
 __device__ __forceinline__ void
 cascade_level(const CascadeParams& p,
               const T (&in)[RI][CI],
@@ -472,7 +704,14 @@ cascade_level(const CascadeParams& p,
                                       row0 >> (J - 1));
     T* dst = reinterpret_cast<T*>(p.dst[J - 1]) +
              uint64_t(f) * p.dst_frame_elems[J - 1];
-    if constexpr (STAGED) {
+    if constexpr (TILED) {
+        // a row-major copy only where the next launch reads this level
+        if (p.dst[J - 1])
+            store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
+                                                    col0, row0, lane);
+        store_level_tiled<T, C, J, RO, CO, EDGE>(p, out, f, col0 - uint32_t(lane) * C, row0,
+                                                 lane);
+    } else if constexpr (STAGED) {
         if ((sc->mask >> (J - 1)) & 1u) {
             // the band's rows start at row0 - row0 % 2^NL: one band per block
             stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
@@ -486,8 +725,8 @@ cascade_level(const CascadeParams& p,
                                                 col0, row0, lane);
     }
     if constexpr (J < NL) {
-        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE, NTS, STAGED>(p, out, f, row0,
-                                                                    col0, lane, sc);
+        cascade_level<T, M, C, J + 1, NL, RO, CO, EDGE, NTS, STAGED, TILED>(p, out, f, row0,
+                                                                           col0, lane, sc);
     }
 }
 
@@ -496,7 +735,7 @@ cascade_level(const CascadeParams& p,
 // streams are marked non-temporal: measured on MI355X (tools/microbench.hip,
 // profiles/r01) the headline batch drops from ~530 to ~475 us with NT stores.
 template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true,
-         bool STAGED = false>
+         bool STAGED = false, bool TILED = false>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
@@ -530,10 +769,14 @@ cascade_unit(const CascadeParams& p,
     // keep every load above the reductions (the scheduler would otherwise
     // hold back the last rows' loads to save registers)
     __builtin_amdgcn_sched_barrier(0);
-    cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS, STAGED>(p, v, f, row0, col0, lane, sc);
+    cascade_level<T, M, C, 1, NL, R, C, EDGE, NTS, STAGED, TILED>(p, v, f, row0, col0, lane,
+                                                                   sc);
 }
 
-template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true>
+// TILED: every level goes out in chunk-tile order (store_level_tiled); waves
+// past total_units zero-fill the tile overhang the grid's blocks do not reach
+// (zero_fill_tiled).
+template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true, bool TILED = false>
 __global__ __launch_bounds__(256) void
 cascade_kernel(CascadeParams p)
 {
@@ -541,8 +784,30 @@ cascade_kernel(CascadeParams p)
     // measured 2-4% faster for f32 than the looped form)
     constexpr int R = 1 << NL;
     const int lane = threadIdx.x & 63;
-    const uint32_t u =
-      blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t blk = blockIdx.x;
+    if constexpr (TILED) {
+        // The first blocks zero-fill the tile overhang (dispatched round-robin
+        // over the XCDs like any blocks); the cascade blocks follow.
+        const uint32_t zb = p.zwaves / 4;
+        if (blk < zb) {
+            zero_fill_tiled<T>(p, blk * 4 + wave, p.zwaves, lane, NL,
+                               p.total_units / (p.units_x * p.units_y));
+            return;
+        }
+        blk -= zb;
+    }
+    if (p.remap) {
+        // XCD-contiguous order ($AQZ_XCD_REMAP=1, off by default): workgroup
+        // i runs on XCD i % 8, so remapping i to (i % 8) * (n / 8) + i / 8
+        // gives XCD x a contiguous eighth of the units (whole frames for
+        // batches of >= 8).  Same-box A/B (profiles/r02/remap_ab.log): +2-4%
+        // for 5472x3648, -1-5% for 3000^2, within noise at the headline.
+        const uint32_t nb8 = p.main_blocks & ~7u;
+        if (blk < nb8)
+            blk = (blk & 7u) * (nb8 >> 3) + (blk >> 3);
+    }
+    const uint32_t u = blk * (blockDim.x >> 6) + wave;
     if (u >= p.total_units)
         return;
     const uint32_t ux = u % p.units_x;
@@ -554,9 +819,9 @@ cascade_kernel(CascadeParams p)
     const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
     // wave-uniform: interior tiles take the edge-free path
     if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
-        cascade_unit<T, M, NL, C, NT, false>(p, f, row0, col0, lane);
+        cascade_unit<T, M, NL, C, NT, false, true, false, TILED>(p, f, row0, col0, lane);
     } else {
-        cascade_unit<T, M, NL, C, NT, true>(p, f, row0, col0, lane);
+        cascade_unit<T, M, NL, C, NT, true, true, false, TILED>(p, f, row0, col0, lane);
     }
 }
 
@@ -859,21 +1124,6 @@ zpair_kernel(T* out, const T* earlier, const T* current, uint64_t n)
 // tile order (zero-padded) plus the scan result, so the host does one
 // contiguous copy per tile and no scan.  Grid: `slices` blocks per tile, one
 // block-wide OR per block.
-
-template<typename T>
-__device__ __forceinline__ bool
-nonzero_bits(T v)
-{
-    if constexpr (sizeof(T) == 8) {
-        uint64_t b;
-        __builtin_memcpy(&b, &v, 8);
-        return b != 0;
-    } else {
-        uint32_t b = 0;
-        __builtin_memcpy(&b, &v, sizeof(T));
-        return b != 0;
-    }
-}
 
 // SLICE_FLAGS: every block writes its own flag byte (flags[t*slices + s]),
 // no atomics and no pre-clear; otherwise one u32 per tile, OR-ed atomically
@@ -1355,6 +1605,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         }
         // 4 waves per block, one tile per wave per iteration.
         const uint32_t grid = grid_for(total, 4, 0);
+        p.main_blocks = grid;
+        p.remap = xcd_remap_env() == 1;
         // Band staging when some level's rows are not whole 64-byte bursts
         // and a row band is at most 4 tiles ($AQZ_BAND_STAGING=0: never).
         // Wider bands would need bigger workgroups, and a workgroup that
@@ -1421,6 +1673,163 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                     default:
                         hipLaunchKernelGGL((cascade_kernel<T, M, 4, C>), dim3(grid), dim3(256),
                                            0, stream, p);
+                        break;
+                }
+            };
+            if (cols == CW)
+                go(std::integral_constant<int, int(CW)>{});
+            else
+                go(std::integral_constant<int, int(CN)>{});
+            return hipGetLastError();
+        });
+    });
+}
+
+#if AQZ_SHARD == 0
+
+uint32_t
+cascade_tiled_cols(int dtype, uint32_t W)
+{
+    // cascade_pick_cols for element-aligned buffers: wide tiles once a wave's
+    // 64 lanes fit in the frame, half-width ones below
+    const size_t b = dtype_bytes(dtype);
+    if (!b)
+        return 0;
+    const uint32_t cw = cascade_cols(b);
+    return W >= 64 * cw ? cw : cw / 2;
+}
+
+uint32_t
+cascade_tiled_slots(int dtype,
+                    uint32_t W,
+                    int n_out,
+                    int level,
+                    uint32_t tile_rows,
+                    uint32_t tile_cols,
+                    uint32_t* slots_x)
+{
+    const uint32_t cols = cascade_tiled_cols(dtype, W);
+    const uint32_t cw = (64u * cols) >> level;       // level columns per wave block
+    const uint32_t rh = (1u << n_out) >> level;      // level rows per wave block
+    if (cols == 0 || level < 1 || level > n_out || tile_rows == 0 || tile_cols == 0 ||
+        tile_cols % cw != 0 || tile_rows % rh != 0) {
+        if (slots_x)
+            *slots_x = 1;
+        return 0;
+    }
+    if (slots_x)
+        *slots_x = tile_cols / cw;
+    return (tile_rows / rh) * (tile_cols / cw);
+}
+#endif
+
+hipError_t
+AQZ_SHARDED(launch_cascade_tiled)(int dtype,
+                                  int method,
+                                  const void* src,
+                                  uint64_t src_frame_elems,
+                                  uint32_t W,
+                                  uint32_t H,
+                                  const LevelOut* outs,
+                                  const TiledOut* touts,
+                                  int n_out,
+                                  uint32_t n_frames,
+                                  hipStream_t stream)
+{
+    const uint32_t cols = cascade_pick_cols(dtype, src, src_frame_elems, W, H, outs, n_out);
+    // the flag layout (cascade_tiled_slots) assumes the geometry-only choice
+    if (cols == 0 || n_frames == 0 || cols != cascade_tiled_cols(dtype, W))
+        return hipErrorInvalidValue;
+    const size_t b = dtype_bytes(dtype);
+    const uint32_t R = 1u << n_out;
+    CascadeParams p{};
+    p.src = static_cast<const uint8_t*>(src);
+    p.src_frame_elems = src_frame_elems;
+    p.W = W;
+    p.H = H;
+    // The grid's blocks cover the frame; zero-fill waves cover the rest of
+    // the padded tile area.
+    p.units_x = (W + 64 * cols - 1) / (64 * cols);
+    p.units_y = (H + R - 1) / R;
+    const uint64_t total = uint64_t(p.units_x) * p.units_y * n_frames;
+    if (total >= (1ull << 30))
+        return hipErrorInvalidValue;
+    p.total_units = uint32_t(total);
+    bool flag_fill = false;
+    for (int i = 0; i < n_out; ++i) {
+        const TiledOut& t = touts[i];
+        if (!t.ptr || t.tile_rows == 0 || t.tile_cols == 0 ||
+            reinterpret_cast<uintptr_t>(t.ptr) % b != 0)
+            return hipErrorInvalidValue;
+        const uint32_t ntx = (outs[i].w + t.tile_cols - 1) / t.tile_cols;
+        const uint32_t nty = (outs[i].h + t.tile_rows - 1) / t.tile_rows;
+        const uint64_t pw = uint64_t(ntx) * t.tile_cols, ph = uint64_t(nty) * t.tile_rows;
+        if (pw >= (1ull << 31) || ph >= (1ull << 31))
+            return hipErrorInvalidValue;
+        p.dst[i] = static_cast<uint8_t*>(outs[i].ptr);
+        p.dst_frame_elems[i] = outs[i].frame_elems;
+        p.w[i] = outs[i].w;
+        p.h[i] = outs[i].h;
+        p.tdst[i] = static_cast<uint8_t*>(t.ptr);
+        p.tframe_elems[i] = pw * ph;
+        p.tr[i] = t.tile_rows;
+        p.tc[i] = t.tile_cols;
+        p.ntx[i] = ntx;
+        p.pw[i] = uint32_t(pw);
+        p.ph[i] = uint32_t(ph);
+        p.cov_w[i] = p.units_x * ((64u * cols) >> (i + 1));
+        p.cov_h[i] = p.units_y * (R >> (i + 1));
+        p.zrows[i] = p.cov_w[i] < pw ? uint32_t(ph)
+                                      : (p.cov_h[i] < ph ? uint32_t(ph) - p.cov_h[i] : 0u);
+        p.zitems += p.zrows[i];
+        p.slots[i] = cascade_tiled_slots(dtype, W, n_out, i + 1, t.tile_rows, t.tile_cols,
+                                         &p.slots_x[i]);
+        p.flags[i] = t.nonzero;
+        p.flags_frame[i] = ntx * nty * std::max<uint32_t>(1, p.slots[i]);
+        if (t.nonzero && p.slots[i] && (p.cov_w[i] < pw || p.cov_h[i] < ph))
+            flag_fill = true;
+        if (t.nonzero && !p.slots[i]) {
+            // one flag per tile, OR-ed by plain stores of 1: cleared first
+            const hipError_t e =
+              hipMemsetAsync(t.nonzero, 0, size_t(n_frames) * ntx * nty, stream);
+            if (e != hipSuccess)
+                return e;
+        }
+    }
+    // zero-fill waves: a whole number of 8-block (one per XCD) groups
+    const uint64_t zitems = uint64_t(p.zitems) * n_frames;
+    p.zwaves = (zitems || flag_fill)
+                 ? uint32_t(std::min<uint64_t>(std::max<uint64_t>(zitems, 64), 4096))
+                 : 0u;
+    p.zwaves = (p.zwaves + 31) & ~31u;
+    p.main_blocks = grid_for(total, 4, 0);
+    p.remap = xcd_remap_env() == 1;
+    const uint32_t grid = p.zwaves / 4 + p.main_blocks;
+
+    return with_dtype(dtype, [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        constexpr uint32_t CW = kCascadeCols<T>;
+        constexpr uint32_t CN = CW / 2;
+        return with_method(method, [&](auto mtag) -> hipError_t {
+            constexpr int M = decltype(mtag)::value;
+            auto go = [&](auto ctag) {
+                constexpr int C = decltype(ctag)::value;
+                switch (n_out) {
+                    case 1:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, true, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                        break;
+                    case 2:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, true, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                        break;
+                    case 3:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, true, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                        break;
+                    default:
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, true, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
                         break;
                 }
             };

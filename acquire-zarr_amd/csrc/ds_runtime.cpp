@@ -134,6 +134,10 @@ struct aqz_ds
     // aqz_ds_take_frame_tiled: on-demand scratch (tiles, then slice flags)
     void* d_tiles = nullptr;
     size_t d_tiles_bytes = 0;
+    // aqz_ds_run_device_batch_tiled: row-major copy of the last level of a
+    // fused run that feeds the next run (pyramids deeper than 4 XY levels)
+    void* d_chain = nullptr;
+    size_t d_chain_bytes = 0;
     // aqz_ds_set_level_tiling: per level (tile_rows, tile_cols), two tiled
     // slots (tiles then slice flags) paired with `slot`, and which slot's
     // frame they currently hold (-1 none)
@@ -273,6 +277,7 @@ tile_to_host(aqz_ds* ds, const void* d_frame, const aqz_level_desc& lv, uint32_t
 {
     if (ds->d_tiles_bytes < g.tile_bytes) {
         (void)hipFree(ds->d_tiles);
+    (void)hipFree(ds->d_chain);
         ds->d_tiles = nullptr;
         ds->d_tiles_bytes = 0;
         HIP_TRY(ds, hipMalloc(&ds->d_tiles, g.tile_bytes), "hipMalloc tiles");
@@ -1288,38 +1293,38 @@ aqz_ds_run_device_batch(aqz_ds* ds,
                                     std::to_string(l));
         if (int rc = bind_device(ds))
             return rc;
-        // A batch on the caller's stream continues the handle's own stream
-        // order: the per-frame fallback reads and writes state (the stored Z
-        // plane, level slots) that earlier add_frame calls left queued on
-        // ds->stream, and later add_frame calls must see what the batch wrote.
-        // The guard joins the two streams both ways and restores ds->stream on
+        // The batch runs on the caller's stream.  The fused paths touch only
+        // the caller's buffers; the per-frame fallback reads and writes the
+        // handle's device state (the stored Z plane, level slots) that earlier
+        // add_frame calls left queued on ds->stream, and later add_frame calls
+        // must see what it wrote.  So the fallback joins the two streams both
+        // ways (joining on every batch put a cross-stream wait in front of
+        // each fused launch), and the guard restores ds->stream on
         // every exit, exceptions included.
         struct StreamSwap
         {
             aqz_ds* ds;
             hipStream_t saved, user;
-            hipError_t enter()
+            bool joined = false;
+            void enter() { ds->stream = user ? user : saved; }
+            hipError_t join()
             {
                 if (!user || user == saved)
                     return hipSuccess;
                 hipError_t e = hipEventRecord(ds->join, saved);
                 if (e == hipSuccess)
                     e = hipStreamWaitEvent(user, ds->join, 0);
-                if (e == hipSuccess)
-                    ds->stream = user;
+                joined = e == hipSuccess;
                 return e;
             }
             ~StreamSwap()
             {
-                if (ds->stream != saved) {
-                    if (hipEventRecord(ds->join, ds->stream) == hipSuccess)
-                        (void)hipStreamWaitEvent(saved, ds->join, 0);
-                    ds->stream = saved;
-                }
+                if (joined && hipEventRecord(ds->join, ds->stream) == hipSuccess)
+                    (void)hipStreamWaitEvent(saved, ds->join, 0);
+                ds->stream = saved;
             }
         } swap{ ds, ds->stream, static_cast<hipStream_t>(hip_stream) };
-        if (hipError_t e = swap.enter(); e != hipSuccess)
-            return ds->fail(e, "run_device_batch: stream join");
+        swap.enter();
 
         std::vector<uint32_t> emitted(ds->n, 0);
         int rc = AQZ_OK;
@@ -1425,6 +1430,8 @@ aqz_ds_run_device_batch(aqz_ds* ds,
             ds->last_batch_kind = volume ? 2 : (all_fused ? 1 : 3);
         } else {
             ds->last_batch_kind = 0;
+            if (hipError_t e = swap.join(); e != hipSuccess)
+                return ds->fail(e, "run_device_batch: stream join");
             Sink sink;
             sink.batch = true;
             sink.out = device_out_levels;
@@ -1440,6 +1447,114 @@ aqz_ds_run_device_batch(aqz_ds* ds,
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
     }
+}
+
+int
+aqz_ds_run_device_batch_tiled(aqz_ds* ds,
+                              const void* device_frames,
+                              uint32_t n_frames,
+                              const uint32_t* tile_rows,
+                              const uint32_t* tile_cols,
+                              void* const* device_out_levels,
+                              uint8_t* const* device_tile_nonzero,
+                              uint32_t* out_counts,
+                              void* hip_stream)
+{
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (ds->transpose)
+            return ds->fail_arg("run_device_batch_tiled: input transposition applies to the "
+                                "per-frame path only");
+        ds->last_input = nullptr;
+        if (!device_frames || !device_out_levels || !tile_rows || !tile_cols)
+            return ds->fail_arg("run_device_batch_tiled: null argument");
+        if (ds->n < 2)
+            return ds->fail_arg("run_device_batch_tiled: the pyramid has no level to tile");
+        for (uint32_t l = 1; l < ds->n; ++l) {
+            if (!ds->xy[l] || ds->zh[l])
+                return ds->fail_arg("run_device_batch_tiled: pure-XY (2-D) pyramids only; "
+                                    "level " + std::to_string(l) + " does not halve XY alone");
+            if (!device_out_levels[l] || !tile_rows[l] || !tile_cols[l])
+                return ds->fail_arg("run_device_batch_tiled: level " + std::to_string(l) +
+                                    " needs an output and a nonzero tile shape");
+        }
+        if (int rc = bind_device(ds))
+            return rc;
+        hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ds->stream;
+
+        // Runs of up to kMaxFusedLevels levels; a run that feeds another also
+        // writes its last level row-major into one half of d_chain (the runs
+        // alternate halves, so a run never reads the half it writes).  The
+        // first chained level is the largest: 1/256 of the base after 4 levels.
+        const uint32_t first_feed = aqz::kMaxFusedLevels;
+        if (first_feed + 1 < ds->n) {
+            const size_t half = size_t(n_frames) * ds->bytes[first_feed];
+            if (ds->d_chain_bytes < 2 * half) {
+                HIP_TRY(ds, hipStreamSynchronize(stream), "hipStreamSynchronize");
+                (void)hipFree(ds->d_chain);
+                ds->d_chain = nullptr;
+                ds->d_chain_bytes = 0;
+                HIP_TRY(ds, hipMalloc(&ds->d_chain, 2 * half), "hipMalloc chain");
+                ds->d_chain_bytes = 2 * half;
+            }
+        }
+        const void* src = device_frames;
+        for (uint32_t L = 1, run = 0; L < ds->n; ++run) {
+            const uint32_t k = std::min<uint32_t>(ds->n - L, aqz::kMaxFusedLevels);
+            const bool feeds = L + k < ds->n;
+            aqz::LevelOut o[aqz::kMaxFusedLevels];
+            aqz::TiledOut t[aqz::kMaxFusedLevels];
+            for (uint32_t j = 0; j < k; ++j) {
+                o[j] = { nullptr, elems(ds, L + j), ds->lv[L + j].width, ds->lv[L + j].height };
+                t[j] = { device_out_levels[L + j], tile_rows[L + j], tile_cols[L + j],
+                         device_tile_nonzero ? device_tile_nonzero[L + j] : nullptr };
+            }
+            void* chain = static_cast<uint8_t*>(ds->d_chain) + (run & 1) * (ds->d_chain_bytes / 2);
+            if (feeds)
+                o[k - 1].ptr = chain;
+            const aqz_level_desc& a = ds->lv[L - 1];
+            if (!aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width, a.height, o,
+                                        int(k)))
+                return ds->fail_arg("run_device_batch_tiled: level " + std::to_string(L - 1) +
+                                    " is narrower than one vector load (" +
+                                    std::to_string(a.width) + " px)");
+            const hipError_t e =
+              aqz::launch_cascade_tiled(ds->dtype, ds->method, src, elems(ds, L - 1), a.width,
+                                        a.height, o, t, int(k), n_frames, stream);
+            if (e != hipSuccess)
+                return e == hipErrorInvalidValue
+                         ? ds->fail_arg("run_device_batch_tiled: unsupported geometry")
+                         : ds->fail(e, "batch tiled cascade");
+            src = chain;
+            L += k;
+        }
+        for (uint32_t l = 0; l < ds->n; ++l) {
+            ds->count[l] += n_frames;
+            if (out_counts)
+                out_counts[l] = n_frames;
+        }
+        ds->last_batch_kind = 4;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
+}
+
+uint32_t
+aqz_ds_tiled_flag_slots(const aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t tile_cols)
+{
+    if (!ds || level == 0 || level >= ds->n || tile_rows == 0 || tile_cols == 0)
+        return 0;
+    // the fused run holding `level`: levels 1-4, 5-8, ... (kMaxFusedLevels)
+    const uint32_t start = 1 + ((level - 1) / aqz::kMaxFusedLevels) * aqz::kMaxFusedLevels;
+    const uint32_t k = std::min<uint32_t>(ds->n - start, aqz::kMaxFusedLevels);
+    const uint32_t s = aqz::cascade_tiled_slots(ds->dtype, ds->lv[start - 1].width, int(k),
+                                                int(level - start + 1), tile_rows, tile_cols,
+                                                nullptr);
+    return s ? s : 1;
 }
 
 namespace {

@@ -119,20 +119,27 @@ def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
         q.wait()
 
 
-def algorithmic_bytes(geo, counts, frames: int, method: str, bpp: int):
+def algorithmic_bytes(geo, counts, frames: int, method: str, bpp: int, tile=None):
     """(read, read + written) algorithmic bytes of one batch step (SURVEY
     §8(d)): every input frame read once, every emitted level frame
-    (counts[L] of level L) written once.  Decimate keeps the top-left pixel
-    and the earlier plane, so only the even rows (and, where level 1 halves
-    Z, the even planes) are needed; whole rows, because the sampled columns
-    share 64-B bursts with the skipped ones.  Every other method reads all."""
+    (counts[L] of level L) written once — with `tile` = (rows, cols), as
+    whole chunk tiles, zero overhang included.  Decimate keeps the top-left
+    pixel and the earlier plane, so only the even rows (and, where level 1
+    halves Z, the even planes) are needed; whole rows, because the sampled
+    columns share 64-B bursts with the skipped ones.  Every other method
+    reads all."""
     W, H, planes0 = geo[0]
     read = frames * W * H * bpp
     if method == "decimate" and len(geo) > 1:
         rows = (H + 1) // 2 if geo[1][0] < W or geo[1][1] < H else H
         planes = (frames + 1) // 2 if geo[1][2] < planes0 else frames
         read = planes * rows * W * bpp
-    written = sum(counts[L] * geo[L][0] * geo[L][1] * bpp for L in range(1, len(geo)))
+    if tile:
+        tr, tc = tile
+        written = sum(counts[L] * (-(-geo[L][0] // tc)) * (-(-geo[L][1] // tr)) * tr * tc * bpp
+                      for L in range(1, len(geo)))
+    else:
+        written = sum(counts[L] * geo[L][0] * geo[L][1] * bpp for L in range(1, len(geo)))
     return read, read + written
 
 
@@ -196,6 +203,15 @@ def parse(argv=None):
                    help="N>1 only (BASELINE config F): every step, rank 0 scatters "
                         "the ranks' frames over xGMI with RCCL p2p and gathers "
                         "the levels back; timed end to end")
+    p.add_argument("--tiled", action="store_true",
+                   help="emit every level chunk-tiled (chunk x chunk tiles) from the "
+                        "pyramid kernel itself: aqz_ds_run_device_batch_tiled "
+                        "(SURVEY §8(f) row 2); 2-D workloads")
+    p.add_argument("--no-flags", action="store_true",
+                   help="--tiled without the chunk zero scan (A/B of its cost)")
+    p.add_argument("--shape", default="",
+                   help="WxH: override the workload's frame size (same dtype, chunk "
+                        "and batch bytes), e.g. 5472x3648")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
@@ -232,6 +248,13 @@ def main():
             dist.init_process_group(backend)
 
     W, H, Z, dtype, chunk, zchunk, default_batch = WORKLOADS[args.workload]
+    if args.shape:
+        # same batch bytes as the workload's default batch
+        W2, H2 = (int(x) for x in args.shape.lower().split("x"))
+        default_batch = max(1, default_batch * W * H // (W2 * H2))
+        W, H = W2, H2
+    if args.tiled and Z:
+        raise SystemExit("--tiled: 2-D workloads only")
     method = aqz.METHODS[args.method]
     dims = [(aqz.TIME, 0, 1, 1)]
     if Z:
@@ -251,10 +274,22 @@ def main():
     else:
         d_in = torch.randint(0, 256, (B * frame_bytes,), dtype=torch.uint8,
                              device="cuda", generator=gen)
-    outs = [None] + [torch.empty(B * w * h * bpp, dtype=torch.uint8, device="cuda")
-                     for w, h, _ in geo[1:]]
-    out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
     ds = aqz.Downsampler(geo, dtype, method, device=device)
+    if args.tiled:
+        # chunk x chunk tiles per level, zero overhang included
+        tile_elems = [0] + [(-(-w // chunk)) * (-(-h // chunk)) * chunk * chunk
+                            for w, h, _ in geo[1:]]
+        outs = [None] + [torch.empty(B * e * bpp, dtype=torch.uint8, device="cuda")
+                         for e in tile_elems[1:]]
+        flag_slots = [0] + [ds.tiled_flag_slots(L, chunk, chunk) for L in range(1, n_levels)]
+        flags = [None] + [torch.empty(B * e // (chunk * chunk) * flag_slots[L],
+                                      dtype=torch.uint8, device="cuda")
+                          for L, e in enumerate(tile_elems[1:], 1)]
+        flag_ptrs = None if args.no_flags else [0] + [f.data_ptr() for f in flags[1:]]
+    else:
+        outs = [None] + [torch.empty(B * w * h * bpp, dtype=torch.uint8, device="cuda")
+                         for w, h, _ in geo[1:]]
+    out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
     # A real (non-null) stream: the kernels run on it and the timing events
     # are recorded on it.
     torch.cuda.synchronize()  # inputs were generated on the default stream
@@ -282,6 +317,10 @@ def main():
             mine = scatter_frames(pool, d_in, frame_bytes, B, dist, rank, world)
             counts[:] = ds.run_device_batch(mine.data_ptr(), B, out_ptrs, sptr)
             gather_levels(outs, pool_levels, dist, rank, world)
+        elif args.tiled:
+            counts[:] = ds.run_device_batch_tiled(d_in.data_ptr(), B,
+                                                  [None] + [(chunk, chunk)] * (n_levels - 1),
+                                                  out_ptrs, flag_ptrs, sptr)
         else:
             counts[:] = ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
 
@@ -314,8 +353,18 @@ def main():
                     continue
                 w, h, _ = geo[L]
                 k = emitted[L]
-                got = outs[L][k * w * h * bpp:(k + 1) * w * h * bpp].cpu().numpy()
-                ok = ok and np.array_equal(got, r.view(np.uint8).reshape(-1))
+                if args.tiled:
+                    e = tile_elems[L] * bpp
+                    got = outs[L][k * e:(k + 1) * e].cpu().numpy()
+                    t, nz = orc_mod.tile_frame(r, chunk, chunk)
+                    S = flag_slots[L]
+                    ok = ok and np.array_equal(got, t.view(np.uint8).reshape(-1))
+                    if not args.no_flags:
+                        gf = flags[L][k * len(nz) * S:(k + 1) * len(nz) * S].cpu().numpy()
+                        ok = ok and np.array_equal(gf.reshape(len(nz), S).any(axis=1), nz)
+                else:
+                    got = outs[L][k * w * h * bpp:(k + 1) * w * h * bpp].cpu().numpy()
+                    ok = ok and np.array_equal(got, r.view(np.uint8).reshape(-1))
                 emitted[L] += 1
         check = ("bit-exact" if ok else "MISMATCH") + f" ({nchk} frame(s) vs oracle)"
 
@@ -347,9 +396,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
 
-    read_bytes, alg_bytes = algorithmic_bytes(geo, counts, B, args.method, bpp)
-    kind = ds.last_batch_kind()  # 1 fused 2-D cascade, 2 fused volume, 0 per-frame
-    per = {1: 4, 2: 2}.get(kind)  # levels per launch (kind 3: mixed, not derived)
+    read_bytes, alg_bytes = algorithmic_bytes(geo, counts, B, args.method, bpp,
+                                              tile=(chunk, chunk) if args.tiled else None)
+    kind = ds.last_batch_kind()  # 1 fused 2-D cascade, 2 fused volume, 0 per-frame, 4 tiled
+    per = {1: 4, 2: 2, 4: 4}.get(kind)  # levels per launch (kind 3: mixed, not derived)
     launches = -(-(n_levels - 1) // per) if per else None
     avg_launch_s = float(np.mean(launch_ms)) / 1e3
     achieved = alg_bytes / avg_launch_s / 1e9
@@ -410,9 +460,11 @@ def main():
         e2e = {"pipelined_all_ranks": e2e_multi}
 
     if rank == 0:
-        metric = HEADLINE_METRIC if args.workload == "4096x4096_u16" else (
-            f"GPixels/s device-resident multiscale downsample, {args.workload}, "
-            f"{n_levels} levels")
+        metric = HEADLINE_METRIC if (args.workload == "4096x4096_u16" and not args.shape
+                                     and not args.tiled) else (
+            f"GPixels/s device-resident multiscale downsample, {W}x{H} "
+            f"{np.dtype(dtype).name}, {n_levels} levels" +
+            (f", chunk-tiled {chunk}x{chunk}" if args.tiled else ""))
         line = {
             "metric": metric,
             "value": round(value, 2),
@@ -433,7 +485,8 @@ def main():
                        "launches_per_step": launches,
                        "batch_path": {0: "per-frame", 1: "fused cascade",
                                       2: "fused volume",
-                                      3: "batched, partly single-level"}.get(kind, "?"),
+                                      3: "batched, partly single-level",
+                                      4: "fused cascade, chunk-tiled levels"}.get(kind, "?"),
                        "parallelism": (f"rank-0 batch scattered/gathered over xGMI "
                                        f"(RCCL p2p) x{world}" if xgmi else
                                        f"frame-sharded x{world}, no collective")
@@ -625,6 +678,12 @@ def measure_traffic(args, kernel):
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
                "--workload", args.workload, "--batch", str(args.batch),
                "--method", args.method, "--steps", "3", "--warmup", "1"]
+        if args.tiled:
+            cmd.append("--tiled")
+        if args.no_flags:
+            cmd.append("--no-flags")
+        if args.shape:
+            cmd += ["--shape", args.shape]
         env = dict(os.environ, TMPDIR="/tmp")
         try:
             r = subprocess.run(cmd, env=env, capture_output=True, text=True,

@@ -342,6 +342,51 @@ int aqz_ds_run_device_batch(aqz_ds* ds,
                             void* hip_stream);
 
 /*
+ * Device-resident batch with every level emitted chunk-tiled by the pyramid
+ * kernel itself: the k-th frame of level L is written to
+ * `device_out_levels[L] + k * n_tiles(L) * tile_rows[L] * tile_cols[L] *
+ * bytes_of_type` in the order Array::write_frame_to_chunks_ fills chunks
+ * (array.cpp:507-622): tile t = ty * n_tiles_x + tx holds tile_rows[L] x
+ * tile_cols[L] pixels row-major, zero where it overhangs the level — the
+ * bytes Chunk::write_tile_rows (chunk.cpp:17-58) leaves in the tile's slot —
+ * with n_tiles_x = ceil(width / tile_cols[L]) and n_tiles(L) = n_tiles_x *
+ * ceil(height / tile_rows[L]).  `device_tile_nonzero[L]` (optional: the
+ * array or any entry may be NULL) receives the chunk zero scan as
+ * S = aqz_ds_tiled_flag_slots(ds, L, tile_rows[L], tile_cols[L]) flag bytes
+ * per tile (tile-major, n_tiles(L) * S bytes per frame): a tile holds a
+ * nonzero byte iff any of its S bytes is nonzero.  Index 0 of every array is
+ * ignored.  One kernel per 4 levels writes the levels from registers — no
+ * row-major pass, no tiling pass — and its trailing waves zero the tile
+ * overhang; when S > 1 every flag byte is written once by the wave that owns
+ * it, so nothing is cleared first (S == 1: one byte per tile, cleared by a
+ * fill before the kernel).
+ * Pure-XY (2-D) pyramids only, frames at least one 16-byte load wide, no
+ * input transposition; anything else is AQZ_INVALID_ARGUMENT.  Runs on
+ * `hip_stream` (NULL = the handle's stream) without synchronising;
+ * `out_counts` as for aqz_ds_run_device_batch.
+ */
+int aqz_ds_run_device_batch_tiled(aqz_ds* ds,
+                                  const void* device_frames,
+                                  uint32_t n_frames,
+                                  const uint32_t* tile_rows,
+                                  const uint32_t* tile_cols,
+                                  void* const* device_out_levels,
+                                  uint8_t* const* device_tile_nonzero,
+                                  uint32_t* out_counts,
+                                  void* hip_stream);
+
+/*
+ * Flag bytes per tile that aqz_ds_run_device_batch_tiled writes for level
+ * `level` with tile_rows x tile_cols tiles: S > 1 when the kernel's wave
+ * blocks tile the chunk tiles exactly (one byte per block), else 1.  0 for a
+ * bad level or tile shape.
+ */
+uint32_t aqz_ds_tiled_flag_slots(const aqz_ds* ds,
+                                 uint32_t level,
+                                 uint32_t tile_rows,
+                                 uint32_t tile_cols);
+
+/*
  * Host-resident batch, pipelined (overlapping frames).
  * Same results as aqz_ds_add_frame + aqz_ds_take_frame(every level) on each
  * of `n_frames` consecutive frames of `host_frames`: the k-th frame emitted at
@@ -359,11 +404,12 @@ int aqz_ds_run_host_batch(aqz_ds* ds,
                           uint32_t* out_counts);
 
 /*
- * Diagnostic: the path the last aqz_ds_run_device_batch took —
+ * Diagnostic: the path the last aqz_ds_run_device_batch[_tiled] took —
  * 0 = per-frame state machine, 1 = fused 2-D cascade, 2 = fused volume
  * (XY + Z), 3 = 2-D batch with some level runs on batched single-level
  * kernels (frames narrower than one 16-byte load, or buffers that are not
  * element-aligned; the fused kernels take any other width and offset),
+ * 4 = fused 2-D cascade writing chunk tiles (aqz_ds_run_device_batch_tiled),
  * -1 = none.
  */
 int aqz_ds_last_batch_kind(const aqz_ds* ds);
