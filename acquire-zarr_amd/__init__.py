@@ -358,6 +358,37 @@ class Downsampler:
             ctypes.c_void_p(stream) if stream else None))
         return list(counts)
 
+    def batch_call(self, device_frames: int, n_frames: int, device_outs, stream: int = 0,
+                   tiles=None, device_nonzero=None):
+        """A prepared aqz_ds_run_device_batch (or, with `tiles`,
+        aqz_ds_run_device_batch_tiled) call: the ctypes argument arrays are
+        built once, so each call costs one foreign call — what a benchmark
+        loop of short launches needs to keep the stream fed.  Returns a
+        function that runs one batch and returns the per-level counts."""
+        n = self.n_levels
+        L = lib()
+        outs = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in device_outs])
+        counts = (ctypes.c_uint32 * n)()
+        st = ctypes.c_void_p(stream) if stream else None
+        h = self._h
+        if tiles is None:
+            fn, args = L.aqz_ds_run_device_batch, (h, device_frames, n_frames, outs, counts, st)
+        else:
+            tr = (ctypes.c_uint32 * n)(*[int(t[0]) if t else 0 for t in tiles])
+            tc = (ctypes.c_uint32 * n)(*[int(t[1]) if t else 0 for t in tiles])
+            nz = None
+            if device_nonzero is not None:
+                nz = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in device_nonzero])
+            fn = L.aqz_ds_run_device_batch_tiled
+            args = (h, device_frames, n_frames, tr, tc, outs, nz, counts, st)
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                self._check(rc)
+            return counts
+        return call
+
     def tiled_flag_slots(self, level: int, tile_rows: int, tile_cols: int) -> int:
         """Zero-scan flag bytes per tile of run_device_batch_tiled at `level`."""
         return lib().aqz_ds_tiled_flag_slots(self._h, level, tile_rows, tile_cols)

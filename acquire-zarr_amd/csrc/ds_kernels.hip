@@ -280,6 +280,61 @@ load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tai
 
 // ---- fused cascade ---------------------------------------------------------
 
+// Division by a runtime constant as a multiply-high and shifts (Granlund &
+// Montgomery; exact for every 32-bit n).  The tiled stores divide row and
+// column indices by the chunk shape: per block, not per element, but on
+// small frames a block is a few KiB and a 32-bit division's ~40 scalar
+// instructions showed up (512^2 u8 tiled).
+struct FastDiv
+{
+    uint32_t d = 1, m = 0, s = 0; // d == 1: m = 0, q = n
+
+    static FastDiv make(uint32_t d)
+    {
+        FastDiv f;
+        f.d = d ? d : 1;
+        if (f.d == 1)
+            return f;
+        uint32_t l = 0;
+        while ((1ull << l) < f.d)
+            ++l;
+        f.m = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << l) - f.d)) / f.d + 1);
+        f.s = l - 1;
+        return f;
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const
+    {
+        if (d == 1)
+            return n;
+        const uint32_t t = __umulhi(n, m);
+        return (t + ((n - t) >> 1)) >> s;
+    }
+};
+
+// One chunk-tiled output level of the tiled cascade.  Level tiles at
+// tdst + frame * tframe_elems, tile t = ty * ntx + tx, tr x tc elements
+// row-major; the padded level is pw x ph.
+// Zero scan.  slots > 0 (wave blocks and tiles nest): tile t owns `slots`
+// flag bytes, one per (block, tile) pair (slots_x across), and every byte is
+// written exactly once — by its wave, or as 0 by the zero-fill waves for
+// blocks past the grid — so nothing is cleared first.  slots == 0: one byte
+// per tile, cleared before the launch, set to 1 by every wave storing a
+// nonzero byte into the tile.
+// Zero-fill waves (wave ids past the grid's blocks): the padded area the
+// blocks do not reach — columns >= cov_w, and rows >= cov_h — per
+// (frame, level, padded row) item (zrows items per frame here), plus the
+// slot flags of those blocks.
+struct TiledLevel
+{
+    uint8_t* tdst;
+    uint8_t* flags;
+    uint64_t tframe_elems;
+    uint32_t tr, tc, ntx, pw, ph;
+    uint32_t slots, slots_x, flags_frame;
+    uint32_t cov_w, cov_h, zrows;
+    FastDiv dr, dc; // by tr, by tc
+};
+
 struct CascadeParams
 {
     const uint8_t* src;
@@ -292,33 +347,40 @@ struct CascadeParams
     uint64_t dst_frame_elems[kMaxFusedLevels];
     uint32_t w[kMaxFusedLevels];
     uint32_t h[kMaxFusedLevels];
-    // Chunk-tiled outputs (cascade_kernel<..., TILED = true>, launch_cascade_tiled):
-    // level J-1's tiles at tdst + frame * tframe_elems, tile t = ty * ntx + tx,
-    // tr x tc elements row-major; the padded level is pw x ph.  dst[J-1] may
-    // then be null (no row-major copy).
-    uint8_t* tdst[kMaxFusedLevels];
-    uint64_t tframe_elems[kMaxFusedLevels];
-    uint32_t tr[kMaxFusedLevels], tc[kMaxFusedLevels], ntx[kMaxFusedLevels];
-    uint32_t pw[kMaxFusedLevels], ph[kMaxFusedLevels];
-    // Zero scan.  slots[J-1] > 0 (the wave's level-J block always lies in one
-    // tile): tile t owns `slots` flag bytes, one per wave block it holds
-    // (slots_x across), and every slot is written exactly once — by its wave,
-    // or as 0 by the zero-fill waves for blocks past the grid — so nothing is
-    // cleared first.  slots[J-1] == 0: one byte per tile, cleared before the
-    // launch, set to 1 by every wave storing a nonzero byte into the tile.
-    uint8_t* flags[kMaxFusedLevels];
-    uint32_t flags_frame[kMaxFusedLevels];
-    uint32_t slots[kMaxFusedLevels], slots_x[kMaxFusedLevels];
-    // Zero-fill waves (wave ids >= total_units): the padded area the grid's
-    // blocks do not reach — columns >= cov_w, and rows >= cov_h — per
-    // (frame, level, padded row) item, plus the slot flags of those blocks.
-    uint32_t cov_w[kMaxFusedLevels], cov_h[kMaxFusedLevels];
-    uint32_t zrows[kMaxFusedLevels]; // items of the level per frame
+    // Chunk-tiled outputs (cascade_kernel<..., TILED>, launch_cascade_tiled), one
+    // TiledLevel per level; dst[J-1] may then be null (no row-major copy).
+    TiledLevel tl[kMaxFusedLevels];
     uint32_t zitems;                 // items per frame, all levels
+    FastDiv zdiv;                    // by zitems
     uint32_t zwaves;                 // zero-fill waves: the grid's first zwaves / 4 blocks
     uint32_t main_blocks;            // blocks of cascade waves after them
     uint32_t remap;                  // 1: XCD-contiguous block order (cascade_kernel)
+    uint32_t nt;                     // launcher's choice of load policy (load_nt)
 };
+
+// $AQZ_LOAD_NT: 1 / 0 forces the fused cascade's loads with / without the
+// non-temporal hint (A/B only); unset (-1): the launcher decides.
+inline int
+load_nt_env()
+{
+    static const int v = [] {
+        const char* e = std::getenv("AQZ_LOAD_NT");
+        return (e && *e) ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
+// Non-temporal loads unless the frame rows are not whole 128-B lines: there a
+// line straddles two waves' row segments, and without the streaming hint the
+// second wave finds it in L2 (3000^2 u16: 2.7% fewer read requests, 4%
+// faster; aligned rows lose 6% without the hint; profiles/r02/loadnt_ab.log).
+inline uint32_t
+load_nt(uint32_t W, size_t bpp)
+{
+    if (load_nt_env() >= 0)
+        return load_nt_env() != 0;
+    return (uint64_t(W) * bpp) % 128 == 0;
+}
 
 // $AQZ_XCD_REMAP: unset = the launcher's default, 0 = off, 1 = on (A/B only).
 inline int
@@ -465,7 +527,7 @@ nonzero_bits(T x)
 // bytes Chunk::write_tile_rows leaves in an overhanging tile slot
 // (chunk.cpp:17-58) — and positions past the padding are skipped.  `wc0` is
 // the wave's first level-0 column (uniform).  Flags: see CascadeParams.
-template<typename T, int C, int J, int RO, int CO, bool EDGE>
+template<typename T, int C, int J, int RO, int CO, bool EDGE, int MODE>
 __device__ __forceinline__ void
 store_level_tiled(const CascadeParams& p,
                   const T (&out)[RO][CO],
@@ -476,30 +538,36 @@ store_level_tiled(const CascadeParams& p,
 {
     constexpr int SO = kLaneStride<C, J>;
     constexpr int I = J - 1;
-    const uint32_t w = p.w[I], h = p.h[I], tr = p.tr[I], tc = p.tc[I];
-    const uint32_t pw = p.pw[I], ph = p.ph[I];
+    const TiledLevel t = p.tl[I]; // one kernarg block load
+    const uint32_t w = p.w[I], h = p.h[I], tr = t.tr, tc = t.tc;
+    const uint32_t pw = t.pw, ph = t.ph;
     const uint32_t lc = (uint32_t(lane) * C) >> J; // lane's column offset in the block
     const uint32_t bc = wc0 >> J;                    // block's first level column (uniform)
     const uint32_t br = row0 >> J;                   // block's first level row (uniform)
     const uint32_t cout0 = bc + lc;
     const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
     const uint64_t tile_elems = uint64_t(tr) * tc;
-    T* base = reinterpret_cast<T*>(p.tdst[I]) + uint64_t(f) * p.tframe_elems[I];
-    uint8_t* flags = p.flags[I] ? p.flags[I] + uint64_t(f) * p.flags_frame[I] : nullptr;
-    const uint32_t K = p.slots[I];
-    if (K) {
-        // The block lies in one tile: uniform tile coordinates, lane offsets
-        // add to the block's column inside it.
+    T* base = reinterpret_cast<T*>(t.tdst) + uint64_t(f) * t.tframe_elems;
+    uint8_t* flags = t.flags ? t.flags + uint64_t(f) * t.flags_frame : nullptr;
+    auto nested = [&]() {
+        const uint32_t K = t.slots;
+        // Blocks and tiles nest: the block lies in one tile (its columns at
+        // offset bx there), or spans whole tiles side by side (bx = 0).
+        // Row and tile coordinates are wave-uniform; lanes add their column.
+        constexpr uint32_t BW = (64u * C) >> J; // block columns at this level
         if (br >= ph || bc >= pw)
             return; // past the padding (uniform): no tile, no slot
-        const uint32_t ty = br / tr, tx = bc / tc;
-        const uint32_t ry0 = br - ty * tr, cx = bc - tx * tc + lc;
-        T* tile = base + (uint64_t(ty) * p.ntx[I] + tx) * tile_elems;
+        const uint32_t ty = t.dr.div(br), tx0 = t.dc.div(bc);
+        const uint32_t ry0 = br - ty * tr, bx = bc - tx0 * tc;
+        const uint32_t ltx = BW > tc ? t.dc.div(lc) : 0u; // lane's tile within the block
+        const uint32_t cx = bx + lc - ltx * tc;
+        T* tile = base + (uint64_t(ty) * t.ntx + tx0 + ltx) * tile_elems;
+        const bool in_pad = cout0 < pw; // a block spanning tiles may pass the padding
         bool nz = false;
 #pragma unroll
         for (int r = 0; r < RO; ++r) {
             const uint32_t row = br + r;
-            if (!leader)
+            if (!leader || !in_pad)
                 continue;
             T v[CO];
 #pragma unroll
@@ -514,17 +582,25 @@ store_level_tiled(const CascadeParams& p,
             }
             store_vec<T, CO, true>(tile + uint64_t(ry0 + r) * tc + cx, v);
         }
-        const bool any = __ballot(nz) != 0; // every lane reaches the vote
+        const uint64_t votes = __ballot(nz); // every lane reaches the vote
         if (flags && lane == 0) {
-            // the block is RO level rows by 64*C >> J level columns
-            constexpr uint32_t BW = (64u * C) >> J;
-            const uint32_t slot = (ry0 / RO) * p.slots_x[I] + (bc - tx * tc) / BW;
-            flags[(uint64_t(ty) * p.ntx[I] + tx) * K + slot] = any ? 1 : 0;
+            const uint32_t srow = (ry0 / RO) * t.slots_x;
+            uint8_t* f0 = flags + (uint64_t(ty) * t.ntx + tx0) * K + srow;
+            if (BW <= tc) {
+                f0[bx / BW] = votes != 0 ? 1 : 0;
+            } else {
+                // one slot per tile the block spans: the lanes of tile q are
+                // those whose columns fall in [q * tc, (q + 1) * tc)
+                const uint32_t lanes = (tc << J) / C; // lanes per tile (<= 64)
+                const uint64_t m = lanes >= 64 ? ~0ull : ((1ull << lanes) - 1);
+                for (uint32_t q = 0; q * lanes < 64 && tx0 + q < t.ntx; ++q)
+                    f0[uint64_t(q) * K] = ((votes >> (q * lanes)) & m) != 0 ? 1 : 0;
+            }
         }
-        return;
-    }
+    };
+    auto general = [&]() {
     // General geometry: per-row tile coordinates, per-lane tile columns.
-    const uint32_t tx = cout0 / tc;
+    const uint32_t tx = t.dc.div(cout0);
     const uint32_t cx = cout0 - tx * tc;
 #pragma unroll
     for (int r = 0; r < RO; ++r) {
@@ -535,8 +611,8 @@ store_level_tiled(const CascadeParams& p,
         }
         if (!ok)
             continue;
-        const uint32_t ty = row / tr;
-        T* trow = base + uint64_t(ty) * p.ntx[I] * tile_elems + uint64_t(row - ty * tr) * tc;
+        const uint32_t ty = t.dr.div(row);
+        T* trow = base + uint64_t(ty) * t.ntx * tile_elems + uint64_t(row - ty * tr) * tc;
         T v[CO];
         bool rnz = false;
 #pragma unroll
@@ -552,7 +628,7 @@ store_level_tiled(const CascadeParams& p,
         if (cx + CO <= tc) {
             store_vec<T, CO, true>(trow + tx * tile_elems + cx, v);
             if (rnz && flags)
-                flags[ty * p.ntx[I] + tx] = 1;
+                flags[ty * t.ntx + tx] = 1;
         } else {
             // the lane's columns cross a tile edge (tc not a multiple of CO)
 #pragma unroll
@@ -560,45 +636,65 @@ store_level_tiled(const CascadeParams& p,
                 const uint32_t col = cout0 + c;
                 if (col >= pw)
                     continue;
-                const uint32_t ctx = col / tc;
+                const uint32_t ctx = t.dc.div(col);
                 const T one[1] = { v[c] };
                 store_vec<T, 1, true>(trow + ctx * tile_elems + (col - ctx * tc), one);
                 if (flags && nonzero_bits(v[c]))
-                    flags[ty * p.ntx[I] + ctx] = 1;
+                    flags[ty * t.ntx + ctx] = 1;
             }
         }
     }
+
+    };
+    if constexpr (MODE == 1) {
+        nested();
+    } else {
+        // per level: nested blocks keep their clear-free slots
+        if (t.slots)
+            nested();
+        else
+            general();
+    }
 }
 
-// Zero-fill wave `z` of `nz` (tiled cascade): the padded tile area past the
-// grid's blocks, item by item — item = (frame, level, padded row), covering
-// columns [cov_w, pw) of rows < cov_h and whole rows >= cov_h — then the
-// slot flags of the blocks past the grid.  16-byte stores inside each tile's
-// row segment, element stores at the segment ends.
+// Level I's TiledLevel with compile-time kernarg offsets (indexing p.tl with
+// a runtime I would copy the array to scratch).
+__device__ __forceinline__ TiledLevel
+tiled_level(const CascadeParams& p, int I)
+{
+    static_assert(kMaxFusedLevels == 4, "tiled_level");
+    return I == 0 ? p.tl[0] : I == 1 ? p.tl[1] : I == 2 ? p.tl[2] : p.tl[3];
+}
+
 template<typename T>
 __device__ __forceinline__ void
 zero_fill_tiled(const CascadeParams& p, uint32_t z, uint32_t nz, int lane, int n_out,
                 uint32_t n_frames)
 {
     constexpr int E = 16 / int(sizeof(T));
-    const uint64_t items = uint64_t(p.zitems) * n_frames;
-    for (uint64_t it = z; it < items; it += nz) {
-        const uint32_t f = uint32_t(it / p.zitems);
-        uint32_t rem = uint32_t(it - uint64_t(f) * p.zitems);
+    const uint32_t items = p.zitems * n_frames; // < 2^32: checked at launch
+    for (uint32_t it = z; it < items; it += nz) {
+        const uint32_t f = p.zdiv.div(it);
+        uint32_t rem = it - f * p.zitems;
         int I = 0;
-        while (I + 1 < n_out && rem >= p.zrows[I]) {
-            rem -= p.zrows[I];
-            ++I;
+#pragma unroll
+        for (int k = 0; k < kMaxFusedLevels - 1; ++k) {
+            const uint32_t zr = k == 0 ? p.tl[0].zrows : k == 1 ? p.tl[1].zrows : p.tl[2].zrows;
+            if (I == k && I + 1 < n_out && rem >= zr) {
+                rem -= zr;
+                ++I;
+            }
         }
-        const uint32_t tr = p.tr[I], tc = p.tc[I], pw = p.pw[I];
-        const uint32_t cw = min(p.cov_w[I], pw), chh = min(p.cov_h[I], p.ph[I]);
+        const TiledLevel t = tiled_level(p, I);
+        const uint32_t tr = t.tr, tc = t.tc, pw = t.pw;
+        const uint32_t cw = min(t.cov_w, pw), chh = min(t.cov_h, t.ph);
         const uint32_t row = cw < pw ? rem : chh + rem;
         const uint32_t a = row >= chh ? 0u : cw;
         const uint64_t tile_elems = uint64_t(tr) * tc;
-        const uint32_t ty = row / tr;
-        T* trow = reinterpret_cast<T*>(p.tdst[I]) + uint64_t(f) * p.tframe_elems[I] +
-                  uint64_t(ty) * p.ntx[I] * tile_elems + uint64_t(row - ty * tr) * tc;
-        for (uint32_t tx = a / tc; tx * tc < pw; ++tx) {
+        const uint32_t ty = t.dr.div(row);
+        T* trow = reinterpret_cast<T*>(t.tdst) + uint64_t(f) * t.tframe_elems +
+                  uint64_t(ty) * t.ntx * tile_elems + uint64_t(row - ty * tr) * tc;
+        for (uint32_t tx = t.dc.div(a); tx * tc < pw; ++tx) {
             const uint32_t c0 = max(a, tx * tc) - tx * tc; // segment [c0, tc) in the tile row
             T* seg = trow + tx * tile_elems + c0;
             const uint32_t len = tc - c0;
@@ -617,22 +713,26 @@ zero_fill_tiled(const CascadeParams& p, uint32_t z, uint32_t nz, int lane, int n
     }
     // slot flags of blocks no wave of the grid owns (rows >= cov_h or
     // columns >= cov_w at their level)
-    for (int I = 0; I < n_out; ++I) {
-        if (!p.slots[I] || !p.flags[I] || (p.cov_w[I] >= p.pw[I] && p.cov_h[I] >= p.ph[I]))
+#pragma unroll
+    for (int I = 0; I < kMaxFusedLevels; ++I) {
+        if (I >= n_out)
+            break;
+        const TiledLevel t = p.tl[I];
+        if (!t.slots || !t.flags || (t.cov_w >= t.pw && t.cov_h >= t.ph))
             continue;
-        const uint32_t K = p.slots[I], kx = p.slots_x[I], ky = K / kx;
-        const uint32_t bh = p.tr[I] / ky, bw = p.tc[I] / kx; // block size at the level
-        const uint64_t per_frame = p.flags_frame[I];
+        const uint32_t K = t.slots, kx = t.slots_x, ky = K / kx;
+        const uint32_t bh = t.tr / ky, bw = t.tc / kx; // slot size at the level
+        const uint64_t per_frame = t.flags_frame;
         const uint64_t total = per_frame * n_frames;
         for (uint64_t q = uint64_t(z) * 64 + lane; q < total; q += uint64_t(nz) * 64) {
             const uint32_t f = uint32_t(q / per_frame);
             const uint32_t s = uint32_t(q - uint64_t(f) * per_frame);
-            const uint32_t t = s / K, slot = s - t * K;
-            const uint32_t ty = t / p.ntx[I], tx = t - ty * p.ntx[I];
-            const uint32_t r0 = ty * p.tr[I] + (slot / kx) * bh;
-            const uint32_t c0 = tx * p.tc[I] + (slot % kx) * bw;
-            if (r0 >= p.cov_h[I] || c0 >= p.cov_w[I])
-                p.flags[I][q] = 0;
+            const uint32_t tile = s / K, slot = s - tile * K;
+            const uint32_t ty = tile / t.ntx, tx = tile - ty * t.ntx;
+            const uint32_t r0 = ty * t.tr + (slot / kx) * bh;
+            const uint32_t c0 = tx * t.tc + (slot % kx) * bw;
+            if (r0 >= t.cov_h || c0 >= t.cov_w)
+                t.flags[q] = 0;
         }
     }
 }
@@ -684,7 +784,7 @@ stage_level(const StageCtx& sc,
 
 // Level J of the 2-D cascade: reduce, store, recurse to J+1.
 template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
-         bool NTS = false, bool STAGED = false, bool TILED = false>
+         bool NTS = false, bool STAGED = false, int TILED = 0>
 __device__ __forceinline__ void
 cascade_level(const CascadeParams& p,
               const T (&in)[RI][CI],
@@ -709,8 +809,8 @@ cascade_level(const CascadeParams& p,
         if (p.dst[J - 1])
             store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
                                                     col0, row0, lane);
-        store_level_tiled<T, C, J, RO, CO, EDGE>(p, out, f, col0 - uint32_t(lane) * C, row0,
-                                                 lane);
+        store_level_tiled<T, C, J, RO, CO, EDGE, TILED>(p, out, f, col0 - uint32_t(lane) * C,
+                                                        row0, lane);
     } else if constexpr (STAGED) {
         if ((sc->mask >> (J - 1)) & 1u) {
             // the band's rows start at row0 - row0 % 2^NL: one band per block
@@ -735,7 +835,7 @@ cascade_level(const CascadeParams& p,
 // streams are marked non-temporal: measured on MI355X (tools/microbench.hip,
 // profiles/r01) the headline batch drops from ~530 to ~475 us with NT stores.
 template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true,
-         bool STAGED = false, bool TILED = false>
+         bool STAGED = false, int TILED = 0>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
@@ -773,10 +873,10 @@ cascade_unit(const CascadeParams& p,
                                                                    sc);
 }
 
-// TILED: every level goes out in chunk-tile order (store_level_tiled); waves
-// past total_units zero-fill the tile overhang the grid's blocks do not reach
-// (zero_fill_tiled).
-template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true, bool TILED = false>
+// TILED (1: blocks and tiles nest, 2: any chunk shape): every level goes out
+// in chunk-tile order (store_level_tiled); the grid's first blocks zero-fill
+// the tile overhang its cascade blocks do not reach (zero_fill_tiled).
+template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true, int TILED = 0>
 __global__ __launch_bounds__(256) void
 cascade_kernel(CascadeParams p)
 {
@@ -1607,6 +1707,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         const uint32_t grid = grid_for(total, 4, 0);
         p.main_blocks = grid;
         p.remap = xcd_remap_env() == 1;
+        p.nt = load_nt(W, sizeof(T));
         // Band staging when some level's rows are not whole 64-byte bursts
         // and a row band is at most 4 tiles ($AQZ_BAND_STAGING=0: never).
         // Wider bands would need bigger workgroups, and a workgroup that
@@ -1633,8 +1734,9 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         const uint32_t bands = p.units_y * n_frames;
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            auto go = [&](auto ctag) {
+            auto go = [&](auto ctag, auto nttag) {
                 constexpr int C = decltype(ctag)::value;
+                constexpr bool NT = decltype(nttag)::value;
                 if (band) {
                     const dim3 blk(64 * band_waves);
                     switch (n_out) {
@@ -1659,27 +1761,33 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                 }
                 switch (n_out) {
                     case 1:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT>), dim3(grid), dim3(256),
                                            0, stream, p);
                         break;
                     case 2:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT>), dim3(grid), dim3(256),
                                            0, stream, p);
                         break;
                     case 3:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT>), dim3(grid), dim3(256),
                                            0, stream, p);
                         break;
                     default:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT>), dim3(grid), dim3(256),
                                            0, stream, p);
                         break;
                 }
             };
-            if (cols == CW)
-                go(std::integral_constant<int, int(CW)>{});
+            auto go_c = [&](auto nttag) {
+                if (cols == CW)
+                    go(std::integral_constant<int, int(CW)>{}, nttag);
+                else
+                    go(std::integral_constant<int, int(CN)>{}, nttag);
+            };
+            if (p.nt)
+                go_c(std::true_type{});
             else
-                go(std::integral_constant<int, int(CN)>{});
+                go_c(std::false_type{});
             return hipGetLastError();
         });
     });
@@ -1711,15 +1819,24 @@ cascade_tiled_slots(int dtype,
     const uint32_t cols = cascade_tiled_cols(dtype, W);
     const uint32_t cw = (64u * cols) >> level;       // level columns per wave block
     const uint32_t rh = (1u << n_out) >> level;      // level rows per wave block
-    if (cols == 0 || level < 1 || level > n_out || tile_rows == 0 || tile_cols == 0 ||
-        tile_cols % cw != 0 || tile_rows % rh != 0) {
-        if (slots_x)
-            *slots_x = 1;
-        return 0;
-    }
+    const uint32_t co = std::max(1u, cols >> level); // columns per lane store
     if (slots_x)
-        *slots_x = tile_cols / cw;
-    return (tile_rows / rh) * (tile_cols / cw);
+        *slots_x = 1;
+    if (cols == 0 || level < 1 || level > n_out || tile_rows == 0 || tile_cols == 0 ||
+        tile_rows % rh != 0)
+        return 0;
+    // blocks inside tiles: one slot per block; blocks spanning whole tiles
+    // (and lane stores inside one tile): one slot per (tile, block row)
+    uint32_t sx = 0;
+    if (tile_cols % cw == 0)
+        sx = tile_cols / cw;
+    else if (cw % tile_cols == 0 && tile_cols % co == 0)
+        sx = 1;
+    if (sx == 0)
+        return 0;
+    if (slots_x)
+        *slots_x = sx;
+    return (tile_rows / rh) * sx;
 }
 #endif
 
@@ -1756,6 +1873,7 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         return hipErrorInvalidValue;
     p.total_units = uint32_t(total);
     bool flag_fill = false;
+    bool nested = true; // every level's wave blocks and tiles nest: mode 1
     for (int i = 0; i < n_out; ++i) {
         const TiledOut& t = touts[i];
         if (!t.ptr || t.tile_rows == 0 || t.tile_cols == 0 ||
@@ -1770,25 +1888,29 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         p.dst_frame_elems[i] = outs[i].frame_elems;
         p.w[i] = outs[i].w;
         p.h[i] = outs[i].h;
-        p.tdst[i] = static_cast<uint8_t*>(t.ptr);
-        p.tframe_elems[i] = pw * ph;
-        p.tr[i] = t.tile_rows;
-        p.tc[i] = t.tile_cols;
-        p.ntx[i] = ntx;
-        p.pw[i] = uint32_t(pw);
-        p.ph[i] = uint32_t(ph);
-        p.cov_w[i] = p.units_x * ((64u * cols) >> (i + 1));
-        p.cov_h[i] = p.units_y * (R >> (i + 1));
-        p.zrows[i] = p.cov_w[i] < pw ? uint32_t(ph)
-                                      : (p.cov_h[i] < ph ? uint32_t(ph) - p.cov_h[i] : 0u);
-        p.zitems += p.zrows[i];
-        p.slots[i] = cascade_tiled_slots(dtype, W, n_out, i + 1, t.tile_rows, t.tile_cols,
-                                         &p.slots_x[i]);
-        p.flags[i] = t.nonzero;
-        p.flags_frame[i] = ntx * nty * std::max<uint32_t>(1, p.slots[i]);
-        if (t.nonzero && p.slots[i] && (p.cov_w[i] < pw || p.cov_h[i] < ph))
+        TiledLevel& q = p.tl[i];
+        q.tdst = static_cast<uint8_t*>(t.ptr);
+        q.tframe_elems = pw * ph;
+        q.tr = t.tile_rows;
+        q.tc = t.tile_cols;
+        q.dr = FastDiv::make(t.tile_rows);
+        q.dc = FastDiv::make(t.tile_cols);
+        q.ntx = ntx;
+        q.pw = uint32_t(pw);
+        q.ph = uint32_t(ph);
+        q.cov_w = p.units_x * ((64u * cols) >> (i + 1));
+        q.cov_h = p.units_y * (R >> (i + 1));
+        q.zrows = q.cov_w < pw ? uint32_t(ph) : (q.cov_h < ph ? uint32_t(ph) - q.cov_h : 0u);
+        p.zitems += q.zrows;
+        q.slots = cascade_tiled_slots(dtype, W, n_out, i + 1, t.tile_rows, t.tile_cols,
+                                      &q.slots_x);
+        if (!q.slots)
+            nested = false;
+        q.flags = t.nonzero;
+        q.flags_frame = ntx * nty * std::max<uint32_t>(1, q.slots);
+        if (t.nonzero && q.slots && (q.cov_w < pw || q.cov_h < ph))
             flag_fill = true;
-        if (t.nonzero && !p.slots[i]) {
+        if (t.nonzero && !q.slots) {
             // one flag per tile, OR-ed by plain stores of 1: cleared first
             const hipError_t e =
               hipMemsetAsync(t.nonzero, 0, size_t(n_frames) * ntx * nty, stream);
@@ -1798,12 +1920,16 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
     }
     // zero-fill waves: a whole number of 8-block (one per XCD) groups
     const uint64_t zitems = uint64_t(p.zitems) * n_frames;
+    if (zitems >= (1ull << 32))
+        return hipErrorInvalidValue;
+    p.zdiv = FastDiv::make(p.zitems ? p.zitems : 1);
     p.zwaves = (zitems || flag_fill)
                  ? uint32_t(std::min<uint64_t>(std::max<uint64_t>(zitems, 64), 4096))
                  : 0u;
     p.zwaves = (p.zwaves + 31) & ~31u;
     p.main_blocks = grid_for(total, 4, 0);
     p.remap = xcd_remap_env() == 1;
+    p.nt = load_nt(W, b);
     const uint32_t grid = p.zwaves / 4 + p.main_blocks;
 
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
@@ -1812,31 +1938,45 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         constexpr uint32_t CN = CW / 2;
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            auto go = [&](auto ctag) {
+            auto go_m = [&](auto ctag, auto nttag, auto mdtag) {
                 constexpr int C = decltype(ctag)::value;
+                constexpr bool NT = decltype(nttag)::value;
+                constexpr int MD = decltype(mdtag)::value;
                 switch (n_out) {
                     case 1:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, true, true>), dim3(grid),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT, MD>), dim3(grid),
                                            dim3(256), 0, stream, p);
                         break;
                     case 2:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, true, true>), dim3(grid),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT, MD>), dim3(grid),
                                            dim3(256), 0, stream, p);
                         break;
                     case 3:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, true, true>), dim3(grid),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT, MD>), dim3(grid),
                                            dim3(256), 0, stream, p);
                         break;
                     default:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, true, true>), dim3(grid),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT, MD>), dim3(grid),
                                            dim3(256), 0, stream, p);
                         break;
                 }
             };
-            if (cols == CW)
-                go(std::integral_constant<int, int(CW)>{});
+            auto go = [&](auto ctag, auto nttag) {
+                if (nested)
+                    go_m(ctag, nttag, std::integral_constant<int, 1>{});
+                else
+                    go_m(ctag, nttag, std::integral_constant<int, 2>{});
+            };
+            auto go_c = [&](auto nttag) {
+                if (cols == CW)
+                    go(std::integral_constant<int, int(CW)>{}, nttag);
+                else
+                    go(std::integral_constant<int, int(CN)>{}, nttag);
+            };
+            if (p.nt)
+                go_c(std::true_type{});
             else
-                go(std::integral_constant<int, int(CN)>{});
+                go_c(std::false_type{});
             return hipGetLastError();
         });
     });

@@ -207,6 +207,8 @@ def parse(argv=None):
                    help="emit every level chunk-tiled (chunk x chunk tiles) from the "
                         "pyramid kernel itself: aqz_ds_run_device_batch_tiled "
                         "(SURVEY §8(f) row 2); 2-D workloads")
+    p.add_argument("--chunk", type=int, default=0,
+                   help="override the workload's XY chunk size (level planning and --tiled tiles)")
     p.add_argument("--no-flags", action="store_true",
                    help="--tiled without the chunk zero scan (A/B of its cost)")
     p.add_argument("--shape", default="",
@@ -253,6 +255,8 @@ def main():
         W2, H2 = (int(x) for x in args.shape.lower().split("x"))
         default_batch = max(1, default_batch * W * H // (W2 * H2))
         W, H = W2, H2
+    if args.chunk:
+        chunk = args.chunk
     if args.tiled and Z:
         raise SystemExit("--tiled: 2-D workloads only")
     method = aqz.METHODS[args.method]
@@ -312,17 +316,22 @@ def main():
         else:
             pool, pool_levels = None, None
 
+    # one prepared foreign call per step: short launches (small frames) would
+    # otherwise wait on Python building ctypes arrays between them
+    if args.tiled:
+        batch = ds.batch_call(d_in.data_ptr(), B, out_ptrs, sptr,
+                              tiles=[None] + [(chunk, chunk)] * (n_levels - 1),
+                              device_nonzero=flag_ptrs)
+    else:
+        batch = ds.batch_call(d_in.data_ptr(), B, out_ptrs, sptr)
+
     def step():
         if xgmi:
             mine = scatter_frames(pool, d_in, frame_bytes, B, dist, rank, world)
             counts[:] = ds.run_device_batch(mine.data_ptr(), B, out_ptrs, sptr)
             gather_levels(outs, pool_levels, dist, rank, world)
-        elif args.tiled:
-            counts[:] = ds.run_device_batch_tiled(d_in.data_ptr(), B,
-                                                  [None] + [(chunk, chunk)] * (n_levels - 1),
-                                                  out_ptrs, flag_ptrs, sptr)
         else:
-            counts[:] = ds.run_device_batch(d_in.data_ptr(), B, out_ptrs, sptr)
+            counts[:] = batch()
 
     if args.pmc_child:
         # launched under `rocprofv3 --pmc` by measure_traffic(): launches only
@@ -682,6 +691,8 @@ def measure_traffic(args, kernel):
             cmd.append("--tiled")
         if args.no_flags:
             cmd.append("--no-flags")
+        if args.chunk:
+            cmd += ["--chunk", str(args.chunk)]
         if args.shape:
             cmd += ["--shape", args.shape]
         env = dict(os.environ, TMPDIR="/tmp")
