@@ -563,24 +563,24 @@ store_level_tiled(const CascadeParams& p,
         const uint32_t cx = bx + lc - ltx * tc;
         T* tile = base + (uint64_t(ty) * t.ntx + tx0 + ltx) * tile_elems;
         const bool in_pad = cout0 < pw; // a block spanning tiles may pass the padding
+        const bool act = leader && in_pad;
+        // Values (zero past the level) and the vote first, so the flag store
+        // goes out ahead of the block's data stores: a wave with little data
+        // retires only when its last store completes.
+        T v[RO][CO];
         bool nz = false;
 #pragma unroll
         for (int r = 0; r < RO; ++r) {
-            const uint32_t row = br + r;
-            if (!leader || !in_pad)
-                continue;
-            T v[CO];
 #pragma unroll
             for (int c = 0; c < CO; ++c) {
                 T x = out[r][c];
                 if constexpr (EDGE) {
-                    if (row >= h || cout0 + c >= w)
+                    if (br + r >= h || cout0 + c >= w)
                         x = T(0);
                 }
-                v[c] = x;
-                nz = nz || nonzero_bits(x);
+                v[r][c] = x;
+                nz = nz || (act && nonzero_bits(x));
             }
-            store_vec<T, CO, true>(tile + uint64_t(ry0 + r) * tc + cx, v);
         }
         const uint64_t votes = __ballot(nz); // every lane reaches the vote
         if (flags && lane == 0) {
@@ -596,6 +596,11 @@ store_level_tiled(const CascadeParams& p,
                 for (uint32_t q = 0; q * lanes < 64 && tx0 + q < t.ntx; ++q)
                     f0[uint64_t(q) * K] = ((votes >> (q * lanes)) & m) != 0 ? 1 : 0;
             }
+        }
+        if (act) {
+#pragma unroll
+            for (int r = 0; r < RO; ++r)
+                store_vec<T, CO, true>(tile + uint64_t(ry0 + r) * tc + cx, v[r]);
         }
     };
     auto general = [&]() {
