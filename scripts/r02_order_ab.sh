@@ -1,0 +1,18 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT=gpurun_out; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_tiled.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest_tiled.log 2>&1 || { tail -40 $OUT/pytest_tiled.log; exit 1; }
+tail -1 $OUT/pytest_tiled.log
+AQZ_TILED_ORDER=col timeout -k 10 400 python -u -m pytest tests/test_gpu_tiled.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest_tiled_col.log 2>&1 || { tail -40 $OUT/pytest_tiled_col.log; exit 1; }
+tail -1 $OUT/pytest_tiled_col.log
+B="--cpu-seconds 0 --e2e-frames 0 --no-pmc --no-check --steps 30 --warmup 5"
+for rep in 1 2; do
+for args in "" "--tiled" "--shape 3000x3000 --tiled" "--workload 512x512_u8 --tiled" "--workload 2048x2048_u16 --tiled"; do
+  for o in row col; do
+    [ -z "$args" ] && [ $o = col ] && continue
+    AQZ_TILED_ORDER=$o timeout -k 10 200 python bench.py $B $args > $OUT/b.json 2> $OUT/b.err || { echo "FAIL $args"; tail -20 $OUT/b.err; exit 1; }
+    python -c "import json;d=json.load(open('$OUT/b.json'));r=d['roofline'];print('$o','$args'.ljust(36),d['value'],r['avg_launch_us'],r['frac'],r.get('same_mix_ceiling',{}).get('frac_of_ceiling'))" | tee -a $OUT/order_ab.log
+  done
+done
+done
