@@ -14,11 +14,21 @@ gcc -O1 -g $SAN -std=c11 -I"$ROOT/oracle" "$ROOT/tests/sanitize/oracle_fuzz.c" \
 HIPCC=/opt/rocm/bin/hipcc
 HF="-O1 -g -std=c++20 -fPIC --offload-arch=gfx950 -I$ROOT/include -I$ROOT/acquire-zarr_amd/csrc"
 HS="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
-for f in ds_kernels.hip ds_runtime.cpp; do
-  $HIPCC $HF $HS -x hip -c "$ROOT/acquire-zarr_amd/csrc/$f" -o "$OUT/${f%.*}.o"
+# ds_kernels.hip in the library's 8 dtype shards, in parallel (ds_dispatch.cpp
+# routes the launchers), like acquire-zarr_amd/Makefile
+pids=()
+for k in 0 1 2 3 4 5 6 7; do
+  $HIPCC $HF $HS -DAQZ_SHARDS=8 -DAQZ_SHARD=$k -x hip -c "$ROOT/acquire-zarr_amd/csrc/ds_kernels.hip" \
+      -o "$OUT/ds_kernels_s$k.o" &
+  pids+=($!)
 done
+for f in ds_dispatch.cpp ds_runtime.cpp; do
+  $HIPCC $HF $HS -DAQZ_SHARDS=8 -x hip -c "$ROOT/acquire-zarr_amd/csrc/$f" -o "$OUT/${f%.*}.o"
+done
+for p in "${pids[@]}"; do wait "$p"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC -fsanitize=address,undefined \
-    "$OUT/ds_kernels.o" "$OUT/ds_runtime.o" -o "$OUT/libaqz_san.so" -Wl,-rpath,/opt/rocm/lib
+    "$OUT"/ds_kernels_s?.o "$OUT/ds_dispatch.o" "$OUT/ds_runtime.o" -o "$OUT/libaqz_san.so" \
+    -Wl,-rpath,/opt/rocm/lib
 # the driver must use the same (clang) sanitizer runtime as the library
 /opt/rocm/lib/llvm/bin/clang -g -fsanitize=address,undefined -I"$ROOT/include" \
     "$ROOT/tests/sanitize/abi_host.c" "$OUT/libaqz_san.so" \

@@ -47,6 +47,16 @@ main(void)
     int has = 1;
     if (aqz_ds_take_frame(NULL, 1, NULL, 0, NULL, &has) != AQZ_INVALID_ARGUMENT)
         return 11;
+    /* round-2 entry points: null handles are rejected without touching memory */
+    uint32_t tr[3] = { 0, 256, 256 }, tc[3] = { 0, 256, 256 };
+    void* outs[3] = { NULL, NULL, NULL };
+    if (aqz_ds_run_device_batch_tiled(NULL, NULL, 1, tr, tc, outs, NULL, NULL, NULL) !=
+        AQZ_INVALID_ARGUMENT)
+        return 12;
+    if (aqz_ds_tiled_flag_slots(NULL, 1, 256, 256) != 0)
+        return 13;
+    if (aqz_ds_run_device_batch(NULL, NULL, 1, outs, NULL, NULL) != AQZ_INVALID_ARGUMENT)
+        return 14;
     aqz_ds_destroy(NULL);
     printf("abi_host: ok (%s)\n", aqz_version());
     return 0;
