@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace aqz {
 
@@ -129,15 +130,15 @@ shuffle_generic_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ ds
 template<int TS>
 constexpr int kBitGroups = 16 / TS;
 
-template<int TS>
-__global__ __launch_bounds__(256) void
+template<int TS, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES) void
 bitshuffle_vec_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
                       uint32_t n_blocks)
 {
     constexpr int G = kBitGroups<TS>;
     // Per wave: 64 threads x 128 input bytes, one 16-B pad per thread row so
     // the per-thread reads below are bank-conflict free.
-    __shared__ u32x4 stage[4][64][9];
+    __shared__ u32x4 stage[WAVES][64][9];
     const uint32_t ne = run.bs / TS;
     const uint32_t row = ne / 8;          // bytes per bit row
     const uint32_t per_thread = row / G;  // threads per block
@@ -320,6 +321,33 @@ filter_run(int shuffle, uint32_t ts, const uint8_t* src, uint8_t* dst, const Blo
                          (ne / 8) % uint32_t(G) == 0 && run.bs % 16 == 0;
         if (!vec)
             return generic(bitshuffle_generic_kernel);
+        // $AQZ_BITSHUFFLE_WAVES=1|2 (A/B): smaller workgroups (the staging
+        // barrier then spans fewer waves)
+        static const int waves = [] {
+            const char* e = std::getenv("AQZ_BITSHUFFLE_WAVES");
+            const int v = e ? std::atoi(e) : 4;
+            return (v == 1 || v == 2) ? v : 4;
+        }();
+        if (waves != 4) {
+            const uint32_t per = ne / 8 / G;
+            return split_launch(run, n_blocks, per, [&](BlockRun r, uint32_t n, uint32_t) {
+                const uint32_t grid = uint32_t((uint64_t(per) * n + 64 * waves - 1) / (64 * waves));
+                auto go = [&](auto kern) {
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, stream, src, dst, r, n);
+                };
+                if (waves == 1) {
+                    if (ts == 1) go(bitshuffle_vec_kernel<1, 1>);
+                    else if (ts == 2) go(bitshuffle_vec_kernel<2, 1>);
+                    else if (ts == 4) go(bitshuffle_vec_kernel<4, 1>);
+                    else go(bitshuffle_vec_kernel<8, 1>);
+                } else {
+                    if (ts == 1) go(bitshuffle_vec_kernel<1, 2>);
+                    else if (ts == 2) go(bitshuffle_vec_kernel<2, 2>);
+                    else if (ts == 4) go(bitshuffle_vec_kernel<4, 2>);
+                    else go(bitshuffle_vec_kernel<8, 2>);
+                }
+            });
+        }
         return split_launch(run, n_blocks, ne / 8 / G,
                             [&](BlockRun r, uint32_t n, uint32_t grid) {
             switch (ts) {
