@@ -382,6 +382,19 @@ load_nt(uint32_t W, size_t bpp)
     return (uint64_t(W) * bpp) % 128 == 0;
 }
 
+// $AQZ_TILED_ZWAVES: unset = the launcher's count of zero-fill waves, else
+// that count (A/B only; 0 skips the zero fill and leaves the overhang
+// unwritten).
+inline int
+tiled_zwaves_env()
+{
+    static const int v = [] {
+        const char* e = std::getenv("AQZ_TILED_ZWAVES");
+        return (e && *e) ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
 // $AQZ_XCD_REMAP: unset = the launcher's default, 0 = off, 1 = on (A/B only).
 inline int
 xcd_remap_env()
@@ -1928,9 +1941,23 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
     if (zitems >= (1ull << 32))
         return hipErrorInvalidValue;
     p.zdiv = FastDiv::make(p.zitems ? p.zitems : 1);
+    // One zero-fill wave per 128 KiB of overhang (64..4096).  The waves run
+    // first and hold their slots while the cascade blocks start; one per
+    // item (up to 4096) cost 4-5% at 3000^2 and 5472x3648 against 512, and
+    // putting them after the cascade blocks made them the kernel's tail
+    // (profiles/r02/tiled_zero_fill_ab.log).
+    uint64_t zbytes = 0;
+    for (int i = 0; i < n_out; ++i) {
+        const TiledLevel& q = p.tl[i];
+        const uint64_t cw = std::min(q.cov_w, q.pw), chh = std::min(q.cov_h, q.ph);
+        zbytes += (uint64_t(q.pw) * q.ph - cw * chh) * b;
+    }
+    zbytes *= n_frames;
     p.zwaves = (zitems || flag_fill)
-                 ? uint32_t(std::min<uint64_t>(std::max<uint64_t>(zitems, 64), 4096))
+                 ? uint32_t(std::min<uint64_t>(std::max<uint64_t>((zbytes >> 17) + 1, 64), 4096))
                  : 0u;
+    if (const int zw = tiled_zwaves_env(); zw >= 0)
+        p.zwaves = uint32_t(zw); // A/B only: 0 leaves the overhang unwritten
     p.zwaves = (p.zwaves + 31) & ~31u;
     p.main_blocks = grid_for(total, 4, 0);
     p.remap = xcd_remap_env() == 1;

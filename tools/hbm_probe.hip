@@ -46,9 +46,102 @@ mix_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint32_t* sin
     }
 }
 
+// Row-shaped probe: the cascade's read pattern without its arithmetic.  One
+// wave per (frame, 16-row band, 1 KiB row segment) unit, four waves per
+// workgroup; each lane loads 16 B from each of the band's 16 rows at
+// row_bytes pitch (lanes past the row end idle, rows past the frame end
+// skipped) and stores WR x 1 KiB contiguous, in unit order, with
+// nontemporal stores.  At row_bytes = 8192 it is the headline's pattern; at
+// 6000 or 10944 the rows split 128-B lines the way 3000^2 and 5472x3648
+// frames do, so the two rates isolate what the frame pitch alone costs.
+template<bool NTLOAD, int WR>
+__global__ __launch_bounds__(256) void
+rows_kernel(const uint8_t* __restrict__ src, uint32_t row_bytes, uint32_t rows,
+            uint32_t bands, uint32_t segs, uint64_t units, u32x4* __restrict__ dst,
+            uint32_t* sink)
+{
+    const uint64_t u = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (u >= units)
+        return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t seg = uint32_t(u % segs);
+    const uint64_t fb = u / segs;
+    const uint32_t band = uint32_t(fb % bands);
+    const uint64_t frame = fb / bands;
+    const uint32_t col = seg * 1024 + lane * 16;
+    const uint8_t* base = src + (frame * rows + uint64_t(band) * 16) * row_bytes + col;
+    const uint32_t nrows = min(16u, rows - band * 16);
+    u32x4 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        v[r] = u32x4{ 0, 0, 0, 0 };
+        if (col < row_bytes && uint32_t(r) < nrows) {
+            const auto* p = reinterpret_cast<const u32x4*>(base + uint64_t(r) * row_bytes);
+            v[r] = NTLOAD ? __builtin_nontemporal_load(p) : *p;
+        }
+    }
+    if constexpr (WR == 0) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            acc ^= v[r].x ^ v[r].y ^ v[r].z ^ v[r].w;
+        if (acc == 0x12345678u)
+            sink[0] = acc;
+    } else {
+        u32x4* o = dst + u * (64 * WR) + lane;
+#pragma unroll
+        for (int k = 0; k < WR; ++k) {
+            u32x4 a = v[k];
+#pragma unroll
+            for (int j = k + WR; j < 16; j += WR)
+                a ^= v[j];
+            __builtin_nontemporal_store(a, o + k * 64);
+        }
+    }
+}
+
 } // namespace
 
 extern "C" {
+
+// Row-shaped probe (rows_kernel above) over `frames` frames of `rows` rows of
+// `row_bytes` bytes (a multiple of 16), dense.  wr = 0 (read only) or 5
+// (16:5, the cascade's 3:1 mix); `dst` must hold units * wr KiB, units =
+// frames * ceil(rows/16) * ceil(row_bytes/1024).  nt_load picks
+// nontemporal loads.  *moved_bytes = frame bytes read + bytes written.
+int
+aqz_hbm_probe_rows(const void* src, uint32_t row_bytes, uint32_t rows, uint32_t frames,
+                   void* dst, void* sink, int wr, int nt_load, void* stream,
+                   uint64_t* moved_bytes)
+{
+    if (!src || !sink || (wr && !dst) || row_bytes == 0 || row_bytes % 16 || rows == 0 ||
+        frames == 0 || (wr != 0 && wr != 5))
+        return int(hipErrorInvalidValue);
+    const uint32_t bands = (rows + 15) / 16, segs = (row_bytes + 1023) / 1024;
+    const uint64_t units = uint64_t(frames) * bands * segs;
+    const uint64_t blocks = (units + 3) / 4;
+    if (blocks >= (1ull << 31))
+        return int(hipErrorInvalidValue);
+    const auto s = static_cast<hipStream_t>(stream);
+    const auto* in = static_cast<const uint8_t*>(src);
+    auto* out = static_cast<u32x4*>(dst);
+    auto* sk = static_cast<uint32_t*>(sink);
+#define AQZ_ROWS(NT, W)                                                                 \
+    hipLaunchKernelGGL((rows_kernel<NT, W>), dim3(blocks), dim3(256), 0, s, in, row_bytes, \
+                       rows, bands, segs, units, out, sk)
+    if (nt_load && wr)
+        AQZ_ROWS(true, 5);
+    else if (nt_load)
+        AQZ_ROWS(true, 0);
+    else if (wr)
+        AQZ_ROWS(false, 5);
+    else
+        AQZ_ROWS(false, 0);
+#undef AQZ_ROWS
+    if (moved_bytes)
+        *moved_bytes = uint64_t(frames) * rows * row_bytes + units * uint64_t(wr) * 1024;
+    return int(hipGetLastError());
+}
 
 // Moves blocks * RD * 4 KiB in and blocks * WR * 4 KiB out, blocks =
 // src_bytes / (RD * 4 KiB).  `dst` must hold blocks * WR * 4 KiB; `sink`
