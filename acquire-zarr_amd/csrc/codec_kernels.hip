@@ -130,7 +130,31 @@ shuffle_generic_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ ds
 template<int TS>
 constexpr int kBitGroups = 16 / TS;
 
-template<int TS, int WAVES = 4>
+// 32x32 bit-matrix transpose in registers, LSB first: afterwards bit e of
+// a[r] is what bit r of a[e] was.  Five block-swap stages of 16 word pairs.
+__device__ __forceinline__ void
+transpose_bits_32(uint32_t (&a)[32])
+{
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+        const int s = 16 >> st;
+        const uint32_t m = st == 0   ? 0x0000FFFFu
+                           : st == 1 ? 0x00FF00FFu
+                           : st == 2 ? 0x0F0F0F0Fu
+                           : st == 3 ? 0x33333333u
+                                     : 0x55555555u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            if (i & s)
+                continue;
+            const uint32_t t = ((a[i] >> s) ^ a[i + s]) & m;
+            a[i + s] ^= t;
+            a[i] ^= t << s;
+        }
+    }
+}
+
+template<int TS, int WAVES = 4, bool WORDS = true>
 __global__ __launch_bounds__(64 * WAVES) void
 bitshuffle_vec_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, BlockRun run,
                       uint32_t n_blocks)
@@ -170,6 +194,50 @@ bitshuffle_vec_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         v[k] = stage[w][lane][k];
+    if constexpr (WORDS && TS >= 2) {
+        // The thread's 128 B as one 32x32 bit matrix whose transpose holds
+        // every bit row (bit r of element e is bit e of bit row r, LSB first):
+        //  TS = 4: 32 elements, a[e] = element e, row r = a[r];
+        //  TS = 8: 16 elements, a[e] / a[16 + e] = low / high word of element
+        //          e, rows r and 32 + r = low / high half of a[r];
+        //  TS = 2: 64 elements, a[e] = element e | element 32 + e << 16,
+        //          row r = a[r] | a[16 + r] << 32.
+        // About a third of the per-byte gather, transpose and scatter work.
+        uint32_t wd[32];
+        __builtin_memcpy(wd, v, sizeof(wd));
+        uint32_t a[32];
+#pragma unroll
+        for (int e = 0; e < 32; ++e) {
+            if constexpr (TS == 4)
+                a[e] = wd[e];
+            else if constexpr (TS == 8)
+                a[e] = e < 16 ? wd[2 * e] : wd[2 * (e - 16) + 1];
+            else
+                a[e] = (e & 1) ? (wd[e / 2] >> 16) | (wd[16 + e / 2] & 0xFFFF0000u)
+                               : (wd[e / 2] & 0xFFFFu) | (wd[16 + e / 2] << 16);
+        }
+        transpose_bits_32(a);
+        uint8_t* d = dst + base + uint64_t(t) * G;
+        if constexpr (TS == 4) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r)
+                __builtin_nontemporal_store(a[r], reinterpret_cast<uint32_t*>(d + uint64_t(r) * row));
+        } else if constexpr (TS == 8) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                __builtin_nontemporal_store(uint16_t(a[r]),
+                                            reinterpret_cast<uint16_t*>(d + uint64_t(r) * row));
+                __builtin_nontemporal_store(
+                  uint16_t(a[r] >> 16), reinterpret_cast<uint16_t*>(d + uint64_t(32 + r) * row));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_nontemporal_store(uint64_t(a[r]) | (uint64_t(a[16 + r]) << 32),
+                                            reinterpret_cast<uint64_t*>(d + uint64_t(r) * row));
+        }
+        return;
+    }
     uint8_t e[128];
     __builtin_memcpy(e, v, sizeof(e));
     // out[r] collects G bytes of bit row r (byte gi = group gi of this thread)
@@ -332,6 +400,28 @@ filter_run(int shuffle, uint32_t ts, const uint8_t* src, uint8_t* dst, const Blo
             return (v == 1 || v == 2 || v == 4) ? v : 0;
         }();
         const int waves = waves_env ? waves_env : (ts <= 2 ? 1 : 4);
+        // $AQZ_BITSHUFFLE_BYTES=1: the per-byte gather form the word transpose
+        // replaced (A/B only)
+        static const bool bytes_env = [] {
+            const char* e = std::getenv("AQZ_BITSHUFFLE_BYTES");
+            return e && *e == '1';
+        }();
+        if (bytes_env && ts >= 2) {
+            const uint32_t per = ne / 8 / G;
+            const uint32_t wv = ts <= 2 ? 1 : 4;
+            return split_launch(run, n_blocks, per, [&](BlockRun r, uint32_t n, uint32_t) {
+                const uint32_t grid = uint32_t((uint64_t(per) * n + 64 * wv - 1) / (64 * wv));
+                if (ts == 2)
+                    hipLaunchKernelGGL((bitshuffle_vec_kernel<2, 1, false>), dim3(grid), dim3(64),
+                                       0, stream, src, dst, r, n);
+                else if (ts == 4)
+                    hipLaunchKernelGGL((bitshuffle_vec_kernel<4, 4, false>), dim3(grid), dim3(256),
+                                       0, stream, src, dst, r, n);
+                else
+                    hipLaunchKernelGGL((bitshuffle_vec_kernel<8, 4, false>), dim3(grid), dim3(256),
+                                       0, stream, src, dst, r, n);
+            });
+        }
         if (waves != 4) {
             const uint32_t per = ne / 8 / G;
             return split_launch(run, n_blocks, per, [&](BlockRun r, uint32_t n, uint32_t) {

@@ -26,6 +26,14 @@ FILTER_CASES = [
     (4, 65536, 65536 * 2 + 1024, 2),  # f32 chunk blocks + an unstaged leftover
     (8, 65536, 65536 * 2, 2),       # f64: 2-B rows per thread
     (2, 32768, 32768 * 3, 2),       # exactly 256 threads per block
+    # 4- and 8-byte bit shuffle through the 32x32 word transpose: short bit
+    # rows, few threads per block, blocks narrower than a wave
+    (4, 256, 256 * 5, 2),           # 8-B rows: 2 threads per block
+    (4, 384, 384 * 3, 2),           # 12-B rows: 3 threads per block
+    (8, 512, 512 * 3 + 72, 3),      # 8-B rows: 4 threads per block; 72-B leftover copied
+    (8, 256, 256 * 6, 2),           # 4-B rows: 2 threads per block
+    (2, 128 * 3, 128 * 3 * 7, 2),   # u16, 24-B rows: 3 threads per block
+    (4, 4096 * 4, 4096 * 4 * 64, 1),  # a 4096-wide f32 level as 16 KiB blocks
 ]
 
 
