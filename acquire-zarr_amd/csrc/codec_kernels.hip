@@ -389,17 +389,17 @@ filter_run(int shuffle, uint32_t ts, const uint8_t* src, uint8_t* dst, const Blo
                          (ne / 8) % uint32_t(G) == 0 && run.bs % 16 == 0;
         if (!vec)
             return generic(bitshuffle_generic_kernel);
-        // One-wave workgroups for 1- and 2-byte types: the staging barrier
-        // then spans one wave (u16 headline chunks: 91% -> 94% of a same-size
-        // copy); 4-byte and 8-byte types measured the same either way and keep
-        // 4 waves (profiles/r02/bitshuffle_waves_ab.log).  $AQZ_BITSHUFFLE_WAVES
-        // = 1, 2 or 4 overrides (A/B only).
+        // One-wave workgroups for 1-byte types (the staging barrier then
+        // spans one wave), four for the word-transpose types: with the
+        // transpose, u16 runs at 104-106% of a same-size copy with 4 waves
+        // against 94% with one (profiles/r02/bitshuffle_waves_word_transpose.log).
+        // $AQZ_BITSHUFFLE_WAVES = 1, 2 or 4 overrides (A/B only).
         static const int waves_env = [] {
             const char* e = std::getenv("AQZ_BITSHUFFLE_WAVES");
             const int v = e ? std::atoi(e) : 0;
             return (v == 1 || v == 2 || v == 4) ? v : 0;
         }();
-        const int waves = waves_env ? waves_env : (ts <= 2 ? 1 : 4);
+        const int waves = waves_env ? waves_env : (ts == 1 ? 1 : 4);
         // $AQZ_BITSHUFFLE_BYTES=1: the per-byte gather form the word transpose
         // replaced (A/B only)
         static const bool bytes_env = [] {
