@@ -56,9 +56,9 @@ mix_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint32_t* sin
 // frames do, so the two rates isolate what the frame pitch alone costs.
 template<bool NTLOAD, int WR>
 __global__ __launch_bounds__(256) void
-rows_kernel(const uint8_t* __restrict__ src, uint32_t row_bytes, uint32_t rows,
-            uint32_t bands, uint32_t segs, uint64_t units, u32x4* __restrict__ dst,
-            uint32_t* sink)
+rows_kernel(const uint8_t* __restrict__ src, uint32_t row_bytes, uint64_t pitch, uint32_t rows,
+            uint64_t frame_stride, uint32_t bands, uint32_t segs, uint64_t units,
+            u32x4* __restrict__ dst, uint32_t* sink)
 {
     const uint64_t u = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
     if (u >= units)
@@ -69,14 +69,14 @@ rows_kernel(const uint8_t* __restrict__ src, uint32_t row_bytes, uint32_t rows,
     const uint32_t band = uint32_t(fb % bands);
     const uint64_t frame = fb / bands;
     const uint32_t col = seg * 1024 + lane * 16;
-    const uint8_t* base = src + (frame * rows + uint64_t(band) * 16) * row_bytes + col;
+    const uint8_t* base = src + frame * frame_stride + uint64_t(band) * 16 * pitch + col;
     const uint32_t nrows = min(16u, rows - band * 16);
     u32x4 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         v[r] = u32x4{ 0, 0, 0, 0 };
         if (col < row_bytes && uint32_t(r) < nrows) {
-            const auto* p = reinterpret_cast<const u32x4*>(base + uint64_t(r) * row_bytes);
+            const auto* p = reinterpret_cast<const u32x4*>(base + uint64_t(r) * pitch);
             v[r] = NTLOAD ? __builtin_nontemporal_load(p) : *p;
         }
     }
@@ -105,17 +105,20 @@ rows_kernel(const uint8_t* __restrict__ src, uint32_t row_bytes, uint32_t rows,
 extern "C" {
 
 // Row-shaped probe (rows_kernel above) over `frames` frames of `rows` rows of
-// `row_bytes` bytes (a multiple of 16), dense.  wr = 0 (read only) or 5
+// `row_bytes` bytes (a multiple of 16), `pitch` bytes apart (>= row_bytes;
+// twice row_bytes reads every other row, as Decimate does), frames
+// `frame_stride` bytes apart (>= rows * pitch).  wr = 0 (read only) or 5
 // (16:5, the cascade's 3:1 mix); `dst` must hold units * wr KiB, units =
 // frames * ceil(rows/16) * ceil(row_bytes/1024).  nt_load picks
-// nontemporal loads.  *moved_bytes = frame bytes read + bytes written.
+// nontemporal loads.  *moved_bytes = bytes read + bytes written.
 int
-aqz_hbm_probe_rows(const void* src, uint32_t row_bytes, uint32_t rows, uint32_t frames,
-                   void* dst, void* sink, int wr, int nt_load, void* stream,
-                   uint64_t* moved_bytes)
+aqz_hbm_probe_rows(const void* src, uint32_t row_bytes, uint64_t pitch, uint32_t rows,
+                   uint64_t frame_stride, uint32_t frames, void* dst, void* sink, int wr,
+                   int nt_load, void* stream, uint64_t* moved_bytes)
 {
     if (!src || !sink || (wr && !dst) || row_bytes == 0 || row_bytes % 16 || rows == 0 ||
-        frames == 0 || (wr != 0 && wr != 5))
+        frames == 0 || (wr != 0 && wr != 5) || pitch < row_bytes || pitch % 16 ||
+        frame_stride < uint64_t(rows) * pitch)
         return int(hipErrorInvalidValue);
     const uint32_t bands = (rows + 15) / 16, segs = (row_bytes + 1023) / 1024;
     const uint64_t units = uint64_t(frames) * bands * segs;
@@ -128,7 +131,7 @@ aqz_hbm_probe_rows(const void* src, uint32_t row_bytes, uint32_t rows, uint32_t 
     auto* sk = static_cast<uint32_t*>(sink);
 #define AQZ_ROWS(NT, W)                                                                 \
     hipLaunchKernelGGL((rows_kernel<NT, W>), dim3(blocks), dim3(256), 0, s, in, row_bytes, \
-                       rows, bands, segs, units, out, sk)
+                       pitch, rows, frame_stride, bands, segs, units, out, sk)
     if (nt_load && wr)
         AQZ_ROWS(true, 5);
     else if (nt_load)
