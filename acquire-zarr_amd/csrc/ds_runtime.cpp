@@ -145,6 +145,10 @@ struct aqz_ds
     std::vector<std::pair<void*, void*>> tslot;
     std::vector<std::pair<uint8_t*, uint8_t*>> tflags; // pinned, kernel-written
     std::vector<int> tiled_for;
+    // eager tiled readback (aqz_ds::eager): pinned copy of a level's tiles,
+    // queued right behind its tile kernel, and which slot's frame it holds
+    std::vector<uint8_t*> h_tiles;
+    std::vector<int> htile_for;
     uint8_t* h_flags = nullptr; // pinned slice flags for on-demand tiling
     size_t h_flags_bytes = 0;
 
@@ -248,6 +252,19 @@ tile_geom(const aqz_ds* ds, uint32_t L, uint32_t tr, uint32_t tc)
     return { nt, nt * tr * tc * ds->bpp, nt * aqz::tile_slices(tr, tc) };
 }
 
+// One flag per tile: the OR of its slice flags (pinned, kernel-written).
+void
+reduce_slice_flags(const TileGeom& g, const uint8_t* flags, uint8_t* tile_nonzero)
+{
+    const size_t slices = g.flag_bytes / g.n_tiles;
+    for (size_t t = 0; t < g.n_tiles; ++t) {
+        uint8_t any = 0;
+        for (size_t q = 0; q < slices; ++q)
+            any |= flags[t * slices + q];
+        tile_nonzero[t] = any ? 1 : 0;
+    }
+}
+
 // D2H of tiles already laid out on the device, then one flag per tile from
 // its slice flags (pinned, written by the tile kernel).
 int
@@ -258,15 +275,8 @@ tiles_to_host(aqz_ds* ds, const TileGeom& g, const void* d_tiles, const uint8_t*
             hipMemcpyAsync(dst, d_tiles, g.tile_bytes, hipMemcpyDeviceToHost, ds->stream),
             "hipMemcpyAsync D2H");
     HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-    if (tile_nonzero) {
-        const size_t slices = g.flag_bytes / g.n_tiles;
-        for (size_t t = 0; t < g.n_tiles; ++t) {
-            uint8_t any = 0;
-            for (size_t q = 0; q < slices; ++q)
-                any |= flags[t * slices + q];
-            tile_nonzero[t] = any ? 1 : 0;
-        }
-    }
+    if (tile_nonzero)
+        reduce_slice_flags(g, flags, tile_nonzero);
     return AQZ_OK;
 }
 
@@ -277,7 +287,6 @@ tile_to_host(aqz_ds* ds, const void* d_frame, const aqz_level_desc& lv, uint32_t
 {
     if (ds->d_tiles_bytes < g.tile_bytes) {
         (void)hipFree(ds->d_tiles);
-    (void)hipFree(ds->d_chain);
         ds->d_tiles = nullptr;
         ds->d_tiles_bytes = 0;
         HIP_TRY(ds, hipMalloc(&ds->d_tiles, g.tile_bytes), "hipMalloc tiles");
@@ -511,7 +520,24 @@ eager_readback(aqz_ds* ds)
     bool any = false;
     for (uint32_t L = 1; L < ds->n; ++L) {
         const int k = ds->cached[L];
-        if (k < 0 || ds->host_for[L] == k || ds->no_eager[L])
+        if (k < 0)
+            continue;
+        if (ds->no_eager[L]) {
+            // taken tiled: copy the tiles out instead, so the D2H overlaps
+            // whatever the caller does before take_frame_tiled
+            if (ds->h_tiles[L] && ds->tiled_for[L] == k && ds->htile_for[L] != k) {
+                const TileGeom g = tile_geom(ds, L, ds->tiling[L].first, ds->tiling[L].second);
+                void* tb = k == 0 ? ds->tslot[L].first : ds->tslot[L].second;
+                HIP_TRY(ds,
+                        hipMemcpyAsync(ds->h_tiles[L], tb, g.tile_bytes, hipMemcpyDeviceToHost,
+                                       ds->stream),
+                        "hipMemcpyAsync D2H (eager tiles)");
+                ds->htile_for[L] = k;
+                any = true;
+            }
+            continue;
+        }
+        if (ds->host_for[L] == k)
             continue;
         HIP_TRY(ds,
                 hipMemcpyAsync(ds->h_level[L], ds->slot_ptr(L, k), ds->bytes[L],
@@ -621,6 +647,7 @@ release(aqz_ds* ds)
         (void)hipFree(p);
     (void)hipHostFree(ds->h_stage);
     (void)hipFree(ds->d_tiles);
+    (void)hipFree(ds->d_chain);
     for (auto& t : ds->tslot) {
         (void)hipFree(t.first);
         (void)hipFree(t.second);
@@ -631,6 +658,8 @@ release(aqz_ds* ds)
     }
     (void)hipHostFree(ds->h_flags);
     for (uint8_t* h : ds->h_level)
+        (void)hipHostFree(h);
+    for (uint8_t* h : ds->h_tiles)
         (void)hipHostFree(h);
     if (ds->levels_d2h)
         (void)hipEventDestroy(ds->levels_d2h);
@@ -806,6 +835,8 @@ aqz_ds_create(const aqz_level_desc* levels,
         ds->tslot.assign(n_levels, { nullptr, nullptr });
         ds->tflags.assign(n_levels, { nullptr, nullptr });
         ds->tiled_for.assign(n_levels, -1);
+        ds->h_tiles.assign(n_levels, nullptr);
+        ds->htile_for.assign(n_levels, -1);
         ds->h_level.assign(n_levels, nullptr);
         ds->host_for.assign(n_levels, -1);
         ds->no_eager.assign(n_levels, 0);
@@ -1000,6 +1031,7 @@ aqz_ds_take_frame(aqz_ds* ds,
         ds->cached[level] = -1;
         ds->tiled_for[level] = -1;
         ds->host_for[level] = -1;
+        ds->htile_for[level] = -1;
         return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
@@ -1029,6 +1061,9 @@ aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t
         (void)hipHostFree(tf.first);
         (void)hipHostFree(tf.second);
         tf = { nullptr, nullptr };
+        (void)hipHostFree(ds->h_tiles[level]);
+        ds->h_tiles[level] = nullptr;
+        ds->htile_for[level] = -1;
         ds->tiling[level] = { 0, 0 };
         ds->tiled_for[level] = -1;
         ds->no_eager[level] = tile_rows != 0;
@@ -1043,6 +1078,10 @@ aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t
                                   hipHostMallocDefault), "hipHostMalloc flags");
         HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.second), g.flag_bytes,
                                   hipHostMallocDefault), "hipHostMalloc flags");
+        if (ds->eager)
+            HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&ds->h_tiles[level]),
+                                      g.tile_bytes, hipHostMallocDefault),
+                    "hipHostMalloc tile copy");
         ds->tiling[level] = { tile_rows, tile_cols };
         return AQZ_OK;
     } catch (...) {
@@ -1083,7 +1122,15 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
             return rc;
         const int k = ds->cached[level];
         if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
-            ds->tiled_for[level] == k) {
+            ds->tiled_for[level] == k && ds->htile_for[level] == k) {
+            // tiled and copied out when the frame was emitted (eager readback)
+            HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
+            std::memcpy(dst, ds->h_tiles[level], g.tile_bytes);
+            if (tile_nonzero)
+                reduce_slice_flags(g, k == 0 ? ds->tflags[level].first
+                                             : ds->tflags[level].second, tile_nonzero);
+        } else if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
+                   ds->tiled_for[level] == k) {
             // tiled when the frame was emitted (aqz_ds_set_level_tiling)
             if (int rc = tiles_to_host(ds, g,
                                        k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
@@ -1097,6 +1144,7 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
         ds->cached[level] = -1;
         ds->tiled_for[level] = -1;
         ds->host_for[level] = -1;
+        ds->htile_for[level] = -1;
         ds->no_eager[level] = 1; // this caller takes the level tiled
         return AQZ_OK;
     } catch (...) {

@@ -184,3 +184,42 @@ def test_tiled_flag_slots_layout(aqz):
     assert ds.tiled_flag_slots(1, 100, 60) == 1
     assert ds.tiled_flag_slots(0, 256, 256) == 0
     ds.close()
+
+
+def test_tiled_batch_chain_survives_on_demand_takes(aqz, oracle):
+    """A deep tiled batch (its chain scratch allocated), on-demand tiled
+    takes of a streamed frame (which grow the tiling scratch), then the deep
+    batch again: both batches and the takes match the oracle."""
+    geo = halving(2100, 700, 7)
+    rng = np.random.default_rng(29)
+    frames = [rng.integers(0, 256, (700, 2100), dtype=np.uint8) for _ in range(2)]
+    ds = aqz.Downsampler(geo, np.uint8, 1)
+    torch = torch_cuda()
+    for rep in range(2):
+        d_in = to_device(np.stack(frames))
+        outs, shapes = [None], [None]
+        for L, (w, h, _) in enumerate(geo[1:], 1):
+            nt = (-(-h // 8)) * (-(-w // 16))
+            outs.append(empty_device(2 * nt * 8 * 16))
+            shapes.append(nt)
+        ds.run_device_batch_tiled(d_in.data_ptr(), 2, [None] + [(8, 16)] * 6,
+                                  [0] + [o.data_ptr() for o in outs[1:]], None,
+                                  launch_stream())
+        torch.cuda.synchronize()
+        for k, fr in enumerate(frames):
+            ref = oracle.cascade_2d(fr, 7, 1)
+            for L in range(1, 7):
+                t = from_device(outs[L], np.uint8, (2, shapes[L], 8, 16))
+                assert_parity(t[k], oracle.tile_frame(ref[L - 1], 8, 16)[0],
+                              f"rep {rep} frame {k} L{L}")
+        # streamed frame, taken tiled on demand with ever larger tiles
+        ds.add_frame(frames[rep])
+        ref = oracle.cascade_2d(frames[rep], 7, 1)
+        for L, tile in ((1, (64, 64)), (2, (128, 256))):
+            got = ds.take_frame_tiled(L, *tile)
+            want_t, want_nz = oracle.tile_frame(ref[L - 1], *tile)
+            assert_parity(got[0], want_t, f"rep {rep} take L{L}")
+            assert np.array_equal(got[1], want_nz)
+        for L in range(3, 7):
+            ds.take_frame(L)
+    ds.close()
