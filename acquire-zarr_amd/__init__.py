@@ -40,6 +40,8 @@ EXPORTS = (
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
     "aqz_blosc_filter_device", "aqz_crc32c_device", "aqz_tile_slices",
     "aqz_tile_frame_device_sliced",
+    "aqz_blosc_blocksize", "aqz_blosc_frame_from_filtered", "aqz_blosc_ctx_create",
+    "aqz_blosc_ctx_destroy", "aqz_blosc_compress_device", "aqz_blosc_codec_info",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
     "aqz_ds_device",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
@@ -99,6 +101,19 @@ def lib() -> ctypes.CDLL:
     L.aqz_tile_frame_device_sliced.argtypes = [i32, vp, u32, u32, u32, u32, vp, vp, vp]
     L.aqz_blosc_filter_device.argtypes = [ctypes.c_int, u32, u32, vp, sz, u32, vp, vp]
     L.aqz_crc32c_device.argtypes = [vp, sz, sz, u32, vp, vp]
+    L.aqz_blosc_blocksize.argtypes = [ctypes.c_int, u32, sz, ctypes.c_char_p,
+                                      ctypes.POINTER(u32)]
+    L.aqz_blosc_frame_from_filtered.argtypes = [ctypes.c_int, ctypes.c_int, u32,
+                                                ctypes.c_char_p, vp, vp, sz, vp, sz,
+                                                ctypes.POINTER(sz), ctypes.POINTER(ctypes.c_int)]
+    L.aqz_blosc_ctx_create.argtypes = [i32, u32, ctypes.POINTER(vp)]
+    L.aqz_blosc_ctx_destroy.argtypes = [vp]
+    L.aqz_blosc_ctx_destroy.restype = None
+    L.aqz_blosc_compress_device.argtypes = [vp, ctypes.c_int, ctypes.c_int, u32,
+                                            ctypes.c_char_p, vp, sz, u32, vp, sz,
+                                            ctypes.POINTER(sz), vp]
+    L.aqz_blosc_codec_info.argtypes = []
+    L.aqz_blosc_codec_info.restype = ctypes.c_char_p
     L.aqz_ds_add_device_frame.argtypes = [vp, vp, sz]
     L.aqz_ds_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz),
                                     ctypes.POINTER(i32)]
@@ -458,6 +473,83 @@ def blosc_filter_device(shuffle: int, typesize: int, blocksize: int, device_src:
                                    ctypes.c_void_p(stream) if stream else None)
     if rc:
         raise AqzError(rc, L.aqz_last_error().decode())
+
+
+BLOSC_MAX_OVERHEAD = 16  # aqz_blosc.h
+
+
+def _raise_if(rc):
+    if rc:
+        raise AqzError(rc, lib().aqz_last_error().decode())
+
+
+def blosc_blocksize(clevel: int, typesize: int, nbytes: int, cname: str) -> int:
+    """aqz_blosc_blocksize: c-blosc's compute_blocksize for blosc_compress_ctx."""
+    bs = ctypes.c_uint32()
+    _raise_if(lib().aqz_blosc_blocksize(clevel, typesize, nbytes, cname.encode(),
+                                        ctypes.byref(bs)))
+    return bs.value
+
+
+def blosc_frame_from_filtered(clevel: int, shuffle: int, typesize: int, cname: str,
+                              filtered, src=None, destsize: int = -1):
+    """aqz_blosc_frame_from_filtered on host arrays.  Returns (frame bytes,
+    raw_needed); with `src` None and raw_needed set, the frame still lacks
+    the raw chunk after its 16-byte header."""
+    f = np.ascontiguousarray(filtered).view(np.uint8).reshape(-1)
+    s = None if src is None else np.ascontiguousarray(src).view(np.uint8).reshape(-1)
+    n = f.size
+    cap = n + BLOSC_MAX_OVERHEAD if destsize < 0 else destsize
+    dest = np.zeros(max(cap, 1), np.uint8)
+    out, raw = ctypes.c_size_t(), ctypes.c_int()
+    _raise_if(lib().aqz_blosc_frame_from_filtered(
+        clevel, shuffle, typesize, cname.encode(), f.ctypes.data,
+        None if s is None else s.ctypes.data, n, dest.ctypes.data, cap,
+        ctypes.byref(out), ctypes.byref(raw)))
+    return dest[:out.value].tobytes(), bool(raw.value)
+
+
+class BloscContext:
+    """aqz_blosc_ctx: compress_in_place (zarr.common.cpp:106-137) for many
+    device chunk buffers at once."""
+
+    def __init__(self, device: int = 0, n_threads: int = 0):
+        h = ctypes.c_void_p()
+        _raise_if(lib().aqz_blosc_ctx_create(device, n_threads, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().aqz_blosc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compress_device(self, clevel: int, shuffle: int, typesize: int, cname: str,
+                        device_src: int, nbytes: int, n_buffers: int, stream: int = 0,
+                        host_dst=None, dst_stride: int = 0):
+        """Frames of `n_buffers` device chunks of `nbytes`; returns the list of
+        frames (bytes) when `host_dst` is None, else the frame sizes."""
+        stride = dst_stride or nbytes + BLOSC_MAX_OVERHEAD
+        own = host_dst is None
+        if own:
+            host_dst = np.empty(n_buffers * stride, np.uint8)
+        sizes = (ctypes.c_size_t * n_buffers)()
+        _raise_if(lib().aqz_blosc_compress_device(
+            self._h, clevel, shuffle, typesize, cname.encode(), device_src, nbytes,
+            n_buffers, host_dst.ctypes.data, stride, sizes,
+            ctypes.c_void_p(stream) if stream else None))
+        if not own:
+            return list(sizes)
+        return [host_dst[k * stride:k * stride + sizes[k]].tobytes() for k in range(n_buffers)]
+
+
+def blosc_codec_info() -> str:
+    return lib().aqz_blosc_codec_info().decode()
 
 
 def crc32c_device(device_data: int, nbytes: int, stride: int, n_buffers: int,

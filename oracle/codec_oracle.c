@@ -4,8 +4,8 @@
  * loaded by tests/ and bench.py's cpu_baseline legs, never by the product.
  *
  * Both algorithms live in third-party dependencies that are absent from
- * /root/reference and from this image, so they are restated from their
- * published definitions and anchored on the reference's call sites:
+ * /root/reference, so they are restated from their published definitions and
+ * anchored on the reference's call sites:
  *
  *  - blosc shuffle filters: c-blosc, pinned `blosc >= 1.21.5` by
  *    vcpkg.json.  The reference calls blosc_compress_ctx(clevel, shuffle,
@@ -24,11 +24,13 @@
  *    polynomial 0x82F63B78, initial value and final xor 0xFFFFFFFF
  *    (RFC 3720 §12.1, B.4).
  *
- * Parity: neither library is importable or buildable here.  The filters are
- * pinned by hand-derived vectors and by an independent numpy formulation of
- * the published layouts (tests/test_oracle_codecs.py); crc32c by the RFC 3720
- * B.4 test vectors.  Byte identity of whole blosc frames is unpinned (no
- * c-blosc here) — see DESIGN.md.
+ * Parity: the filters are pinned by c-blosc itself — the image carries
+ * c-blosc 1.21.0 (/opt/conda/lib/libblosc.so.1), and for incompressible data
+ * it stores every split raw, i.e. exactly its filtered blocks, which equal
+ * these functions' output (tests/test_blosc_frames.py, oracle/blosc_ref.py);
+ * also by hand-derived vectors and an independent numpy formulation
+ * (tests/test_oracle_codecs.py).  crc32c is pinned by the RFC 3720 B.4 test
+ * vectors (google/crc32c is not in the image).
  */
 #include "codec_oracle.h"
 
