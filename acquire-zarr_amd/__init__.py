@@ -40,6 +40,7 @@ EXPORTS = (
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
     "aqz_blosc_filter_device", "aqz_crc32c_device", "aqz_tile_slices",
     "aqz_tile_frame_device_sliced",
+    "aqz_ds_run_device_batch_chunked", "aqz_chunk_frame_offsets",
     "aqz_blosc_blocksize", "aqz_blosc_frame_from_filtered", "aqz_blosc_ctx_create",
     "aqz_blosc_ctx_destroy", "aqz_blosc_compress_device", "aqz_blosc_codec_info",
     "aqz_ds_level_bytes", "aqz_ds_level_count", "aqz_ds_device_memory_usage",
@@ -67,6 +68,29 @@ class LevelDesc(ctypes.Structure):
     _fields_ = [("width", ctypes.c_uint32),
                 ("height", ctypes.c_uint32),
                 ("planes", ctypes.c_uint32)]
+
+
+class ChunkLattice(ctypes.Structure):
+    """aqz_chunk_lattice (include/aqz_downsampler.h)."""
+    _fields_ = [("device_base", ctypes.c_void_p),
+                ("capacity_bytes", ctypes.c_size_t),
+                ("tile_rows", ctypes.c_uint32),
+                ("tile_cols", ctypes.c_uint32),
+                ("chunk_stride_bytes", ctypes.c_size_t),
+                ("frame_offset_bytes", ctypes.POINTER(ctypes.c_uint64))]
+
+
+def chunk_frame_offsets(dims, bytes_per_px: int, first_frame: int, n_frames: int):
+    """aqz_chunk_frame_offsets: (offsets[n_frames], chunk_bytes, layer_bytes)
+    for storage-order `dims` = [(type, array_size, chunk_size, shard), ...]."""
+    arr = (Dimension * len(dims))(*[Dimension(t, a, c, s, 1.0) for t, a, c, s in dims])
+    offs = (ctypes.c_uint64 * max(n_frames, 1))()
+    cb, lb = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().aqz_chunk_frame_offsets(arr, len(dims), bytes_per_px, first_frame, n_frames,
+                                       offs, ctypes.byref(cb), ctypes.byref(lb))
+    if rc:
+        raise AqzError(rc, lib().aqz_last_error().decode())
+    return list(offs)[:n_frames], cb.value, lb.value
 
 
 _lib = None
@@ -122,6 +146,12 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_run_device_batch_tiled.argtypes = [vp, vp, u32, ctypes.POINTER(u32),
                                                 ctypes.POINTER(u32), ctypes.POINTER(vp),
                                                 ctypes.POINTER(vp), ctypes.POINTER(u32), vp]
+    L.aqz_ds_run_device_batch_chunked.argtypes = [vp, vp, u32, ctypes.POINTER(ChunkLattice),
+                                                  ctypes.POINTER(vp), ctypes.POINTER(u32), vp]
+    L.aqz_chunk_frame_offsets.argtypes = [ctypes.POINTER(Dimension), u32, u32, ctypes.c_uint64,
+                                          u32, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint64)]
     L.aqz_ds_tiled_flag_slots.argtypes = [vp, u32, u32, u32]
     L.aqz_ds_tiled_flag_slots.restype = u32
     L.aqz_ds_take_frame_tiled.argtypes = [vp, u32, u32, u32, vp, sz, vp,
@@ -370,6 +400,28 @@ class Downsampler:
         counts = (ctypes.c_uint32 * n)()
         self._check(lib().aqz_ds_run_device_batch_tiled(
             self._h, device_frames, n_frames, tr, tc, outs, nz, counts,
+            ctypes.c_void_p(stream) if stream else None))
+        return list(counts)
+
+    def run_device_batch_chunked(self, device_frames: int, n_frames: int, lattices,
+                                 device_nonzero=None, stream: int = 0):
+        """aqz_ds_run_device_batch_chunked: `lattices[L]` = (device_base,
+        capacity_bytes, tile_rows, tile_cols, chunk_stride_bytes,
+        frame_offset_bytes list) per level (index 0 ignored)."""
+        n = self.n_levels
+        arr = (ChunkLattice * n)()
+        keep = []
+        for L in range(1, n):
+            base, cap, tr, tc, stride, offs = lattices[L]
+            o = (ctypes.c_uint64 * max(n_frames, 1))(*offs)
+            keep.append(o)
+            arr[L] = ChunkLattice(int(base), cap, tr, tc, stride, o)
+        nz = None
+        if device_nonzero is not None:
+            nz = (ctypes.c_void_p * n)(*[int(p) if p else 0 for p in device_nonzero])
+        counts = (ctypes.c_uint32 * n)()
+        self._check(lib().aqz_ds_run_device_batch_chunked(
+            self._h, device_frames, n_frames, arr, nz, counts,
             ctypes.c_void_p(stream) if stream else None))
         return list(counts)
 

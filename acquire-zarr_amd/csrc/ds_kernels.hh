@@ -75,11 +75,16 @@ hipError_t launch_cascade(int dtype,
 // zero where it overhangs the level — the layout Array::write_frame_to_chunks_
 // fills (array.cpp:507-622, chunk.cpp:17-58).  `nonzero` (optional, device)
 // receives the chunk zero scan as flag bytes (cascade_tiled_slots).
+// Chunk lattice instead (frame_offsets non-null, device): frame k's tile t at
+// ptr + frame_offsets[k] + t * tile_stride elements — every tile straight
+// into its chunk buffer at the frame's place in it.
 struct TiledOut
 {
     void* ptr;
     uint32_t tile_rows, tile_cols;
     uint8_t* nonzero;
+    const uint64_t* frame_offsets = nullptr; // elements, n_frames entries
+    uint64_t tile_stride = 0;                // elements (with frame_offsets)
 };
 
 // Columns per lane launch_cascade_tiled uses for W-wide frames of `dtype`

@@ -311,9 +311,14 @@ struct FastDiv
     }
 };
 
-// One chunk-tiled output level of the tiled cascade.  Level tiles at
-// tdst + frame * tframe_elems, tile t = ty * ntx + tx, tr x tc elements
-// row-major; the padded level is pw x ph.
+// One chunk-tiled output level of the tiled cascade.  Frame f's tile
+// t = ty * ntx + tx (tr x tc elements, row-major; the padded level is pw x ph)
+// at tdst + base(f) + t * tstride, where base(f) = f * tframe_elems and
+// tstride = tr * tc (tiles back to back), or — for a chunk lattice
+// (launch_cascade_tiled with TiledOut::frame_offsets) — base(f) = foff[f] and
+// tstride = the distance between neighbouring chunks: the reference's
+// chunks_[tile + tile_group_offset(f)] at chunk_internal_offset(f)
+// (array.cpp:563-617, array.dimensions.cpp:265-314).
 // Zero scan.  slots > 0 (wave blocks and tiles nest): tile t owns `slots`
 // flag bytes, one per (block, tile) pair (slots_x across), and every byte is
 // written exactly once — by its wave, or as 0 by the zero-fill waves for
@@ -329,11 +334,20 @@ struct TiledLevel
     uint8_t* tdst;
     uint8_t* flags;
     uint64_t tframe_elems;
+    const uint64_t* foff; // per-frame element offsets (chunk lattice), or null
+    uint64_t tstride;     // elements from one tile to the next
     uint32_t tr, tc, ntx, pw, ph;
     uint32_t slots, slots_x, flags_frame;
     uint32_t cov_w, cov_h, zrows;
     FastDiv dr, dc; // by tr, by tc
 };
+
+// Element offset of frame f's tile 0 (wave-uniform f: a scalar load).
+__device__ __forceinline__ uint64_t
+tiled_frame_base(const TiledLevel& t, uint32_t f)
+{
+    return t.foff ? t.foff[f] : uint64_t(f) * t.tframe_elems;
+}
 
 struct CascadeParams
 {
@@ -559,8 +573,8 @@ store_level_tiled(const CascadeParams& p,
     const uint32_t br = row0 >> J;                   // block's first level row (uniform)
     const uint32_t cout0 = bc + lc;
     const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
-    const uint64_t tile_elems = uint64_t(tr) * tc;
-    T* base = reinterpret_cast<T*>(t.tdst) + uint64_t(f) * t.tframe_elems;
+    const uint64_t tile_elems = t.tstride;
+    T* base = reinterpret_cast<T*>(t.tdst) + tiled_frame_base(t, f);
     uint8_t* flags = t.flags ? t.flags + uint64_t(f) * t.flags_frame : nullptr;
     auto nested = [&]() {
         const uint32_t K = t.slots;
@@ -708,9 +722,9 @@ zero_fill_tiled(const CascadeParams& p, uint32_t z, uint32_t nz, int lane, int n
         const uint32_t cw = min(t.cov_w, pw), chh = min(t.cov_h, t.ph);
         const uint32_t row = cw < pw ? rem : chh + rem;
         const uint32_t a = row >= chh ? 0u : cw;
-        const uint64_t tile_elems = uint64_t(tr) * tc;
+        const uint64_t tile_elems = t.tstride;
         const uint32_t ty = t.dr.div(row);
-        T* trow = reinterpret_cast<T*>(t.tdst) + uint64_t(f) * t.tframe_elems +
+        T* trow = reinterpret_cast<T*>(t.tdst) + tiled_frame_base(t, f) +
                   uint64_t(ty) * t.ntx * tile_elems + uint64_t(row - ty * tr) * tc;
         for (uint32_t tx = t.dc.div(a); tx * tc < pw; ++tx) {
             const uint32_t c0 = max(a, tx * tc) - tx * tc; // segment [c0, tc) in the tile row
@@ -1909,6 +1923,10 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         TiledLevel& q = p.tl[i];
         q.tdst = static_cast<uint8_t*>(t.ptr);
         q.tframe_elems = pw * ph;
+        q.foff = t.frame_offsets;
+        q.tstride = t.frame_offsets ? t.tile_stride : uint64_t(t.tile_rows) * t.tile_cols;
+        if (q.tstride < uint64_t(t.tile_rows) * t.tile_cols)
+            return hipErrorInvalidValue;
         q.tr = t.tile_rows;
         q.tc = t.tile_cols;
         q.dr = FastDiv::make(t.tile_rows);

@@ -138,6 +138,15 @@ struct aqz_ds
     // fused run that feeds the next run (pyramids deeper than 4 XY levels)
     void* d_chain = nullptr;
     size_t d_chain_bytes = 0;
+    // aqz_ds_run_device_batch_chunked: per-level frame offsets (elements),
+    // staged in pinned memory and copied to the device on the batch's
+    // stream; two halves used by alternate calls, each guarded by the event
+    // recorded after the batch that read it
+    uint64_t* d_lattice = nullptr;
+    uint64_t* h_lattice = nullptr;
+    size_t lattice_half = 0; // entries per half
+    uint32_t lattice_calls = 0;
+    hipEvent_t lattice_done[2] = { nullptr, nullptr };
     // aqz_ds_set_level_tiling: per level (tile_rows, tile_cols), two tiled
     // slots (tiles then slice flags) paired with `slot`, and which slot's
     // frame they currently hold (-1 none)
@@ -647,6 +656,13 @@ release(aqz_ds* ds)
         (void)hipFree(p);
     (void)hipHostFree(ds->h_stage);
     (void)hipFree(ds->d_tiles);
+    for (hipEvent_t e : ds->lattice_done)
+        if (e) {
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
+    (void)hipFree(ds->d_lattice);
+    (void)hipHostFree(ds->h_lattice);
     (void)hipFree(ds->d_chain);
     for (auto& t : ds->tslot) {
         (void)hipFree(t.first);
@@ -688,6 +704,88 @@ release(aqz_ds* ds)
 } // namespace
 
 extern "C" {
+
+// array.dimensions.cpp:168-178 (bytes_per_chunk_, number_of_chunks_in_memory_)
+// and :232-314 (chunk_lattice_index, tile_group_offset, chunk_internal_offset).
+int
+aqz_chunk_frame_offsets(const aqz_dimension* dims,
+                        uint32_t ndims,
+                        uint32_t bytes_per_px,
+                        uint64_t first_frame,
+                        uint32_t n_frames,
+                        uint64_t* frame_offset_bytes,
+                        uint64_t* chunk_bytes,
+                        uint64_t* layer_bytes)
+{
+    try {
+        if (!dims || ndims < 3 || bytes_per_px == 0 || (n_frames && !frame_offset_bytes)) {
+            aqz::set_last_error("chunk_frame_offsets: invalid argument");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        for (uint32_t i = 0; i < ndims; ++i)
+            if (dims[i].chunk_size_px == 0 || (i > 0 && dims[i].array_size_px == 0)) {
+                aqz::set_last_error("chunk_frame_offsets: zero chunk size, or a zero-size "
+                                    "dimension other than the append dimension");
+                return AQZ_INVALID_ARGUMENT;
+            }
+        const int nd = int(ndims);
+        uint64_t per_chunk = bytes_per_px, chunks_in_layer = 1;
+        for (int i = 0; i < nd; ++i) {
+            per_chunk *= dims[i].chunk_size_px;
+            if (i > 0)
+                chunks_in_layer *= (uint64_t(dims[i].array_size_px) + dims[i].chunk_size_px - 1) /
+                                   dims[i].chunk_size_px;
+        }
+        // lattice strides of every dim (chunks), frames per chunk layer
+        std::vector<uint64_t> strides(nd, 1);
+        for (int i = nd - 1; i > 0; --i)
+            strides[i - 1] =
+              strides[i] * ((uint64_t(dims[i].array_size_px) + dims[i].chunk_size_px - 1) /
+                            dims[i].chunk_size_px);
+        uint64_t layer_frames = dims[0].chunk_size_px;
+        for (int i = 1; i + 2 < nd; ++i)
+            layer_frames *= dims[i].array_size_px;
+        const uint64_t tile_bytes =
+          uint64_t(bytes_per_px) * dims[nd - 1].chunk_size_px * dims[nd - 2].chunk_size_px;
+        auto lattice_index = [&](uint64_t fid, int d) -> uint64_t {
+            uint64_t mod = 1, div = 1;
+            for (int i = d; i < nd - 2; ++i) {
+                mod *= dims[i].array_size_px;
+                div *= (i == d ? dims[i].chunk_size_px : dims[i].array_size_px);
+            }
+            return (fid % mod) / div;
+        };
+        auto internal = [&](uint64_t fid) -> uint64_t {
+            std::vector<uint64_t> astr(nd - 2, 1), cstr(nd - 2, 1);
+            uint64_t off = 0;
+            for (int i = nd - 3; i > 0; --i) {
+                const uint64_t idx =
+                  (fid / astr[i]) % dims[i].array_size_px % dims[i].chunk_size_px;
+                astr[i - 1] = astr[i] * dims[i].array_size_px;
+                cstr[i - 1] = cstr[i] * dims[i].chunk_size_px;
+                off += idx * cstr[i];
+            }
+            off += ((fid / astr[0]) % dims[0].chunk_size_px) * cstr[0];
+            return off * tile_bytes;
+        };
+        const uint64_t layer0 = first_frame / layer_frames;
+        for (uint32_t k = 0; k < n_frames; ++k) {
+            const uint64_t fid = first_frame + k;
+            uint64_t group = 0;
+            for (int i = nd - 3; i > 0; --i)
+                group += lattice_index(fid, i) * strides[i];
+            frame_offset_bytes[k] = (fid / layer_frames - layer0) * chunks_in_layer * per_chunk +
+                                    group * per_chunk + internal(fid);
+        }
+        if (chunk_bytes)
+            *chunk_bytes = per_chunk;
+        if (layer_bytes)
+            *layer_bytes = chunks_in_layer * per_chunk;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
+    }
+}
 
 int
 aqz_plan_levels(const aqz_dimension* dims,
@@ -1497,6 +1595,183 @@ aqz_ds_run_device_batch(aqz_ds* ds,
     }
 }
 
+} // extern "C"
+
+namespace {
+
+// Per-level frame offsets of a chunk-lattice batch into the device (elements),
+// through one half of the pinned staging; returns the device pointers.
+int
+stage_lattice(aqz_ds* ds, const aqz_chunk_lattice* lat, uint32_t n_frames, hipStream_t stream,
+              std::vector<const uint64_t*>* dev, int* half_out)
+{
+    const size_t need = size_t(ds->n) * n_frames;
+    if (ds->lattice_half < need) {
+        for (hipEvent_t e : ds->lattice_done)
+            if (e)
+                HIP_TRY(ds, hipEventSynchronize(e), "hipEventSynchronize lattice");
+        (void)hipFree(ds->d_lattice);
+        (void)hipHostFree(ds->h_lattice);
+        ds->d_lattice = nullptr;
+        ds->h_lattice = nullptr;
+        ds->lattice_half = 0;
+        HIP_TRY(ds, hipMalloc(reinterpret_cast<void**>(&ds->d_lattice), 2 * need * 8),
+                "hipMalloc lattice");
+        HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&ds->h_lattice), 2 * need * 8),
+                "hipHostMalloc lattice");
+        ds->lattice_half = need;
+        for (hipEvent_t& e : ds->lattice_done)
+            if (!e)
+                HIP_TRY(ds, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    }
+    const int half = int(ds->lattice_calls++ & 1);
+    // the batch two calls back read this half: it must have finished
+    HIP_TRY(ds, hipEventSynchronize(ds->lattice_done[half]), "hipEventSynchronize lattice");
+    uint64_t* h = ds->h_lattice + size_t(half) * ds->lattice_half;
+    uint64_t* d = ds->d_lattice + size_t(half) * ds->lattice_half;
+    dev->assign(ds->n, nullptr);
+    for (uint32_t l = 1; l < ds->n; ++l)
+        for (uint32_t k = 0; k < n_frames; ++k)
+            h[size_t(l) * n_frames + k] = lat[l].frame_offset_bytes[k] / ds->bpp;
+    HIP_TRY(ds, hipMemcpyAsync(d, h, need * 8, hipMemcpyHostToDevice, stream), "lattice upload");
+    for (uint32_t l = 1; l < ds->n; ++l)
+        (*dev)[l] = d + size_t(l) * n_frames;
+    *half_out = half;
+    return AQZ_OK;
+}
+
+// aqz_ds_run_device_batch_tiled (lat == nullptr: tiles of a frame back to
+// back, frames back to back) and aqz_ds_run_device_batch_chunked (every tile
+// into its chunk of the lattice).
+int
+run_tiled(aqz_ds* ds,
+          const char* who,
+          const void* device_frames,
+          uint32_t n_frames,
+          const uint32_t* tile_rows,
+          const uint32_t* tile_cols,
+          void* const* device_out_levels,
+          const aqz_chunk_lattice* lat,
+          uint8_t* const* device_tile_nonzero,
+          uint32_t* out_counts,
+          void* hip_stream)
+{
+    const std::string w(who);
+    if (int rc = settle(ds))
+        return rc;
+    if (ds->transpose)
+        return ds->fail_arg(w + ": input transposition applies to the per-frame path only");
+    ds->last_input = nullptr;
+    if (!device_frames || (!lat && (!device_out_levels || !tile_rows || !tile_cols)))
+        return ds->fail_arg(w + ": null argument");
+    if (ds->n < 2)
+        return ds->fail_arg(w + ": the pyramid has no level to tile");
+    for (uint32_t l = 1; l < ds->n; ++l) {
+        if (!ds->xy[l] || ds->zh[l])
+            return ds->fail_arg(w + ": pure-XY (2-D) pyramids only; level " + std::to_string(l) +
+                                " does not halve XY alone");
+        const uint32_t tr = lat ? lat[l].tile_rows : tile_rows[l];
+        const uint32_t tc = lat ? lat[l].tile_cols : tile_cols[l];
+        const void* out = lat ? lat[l].device_base : device_out_levels[l];
+        if (!out || !tr || !tc)
+            return ds->fail_arg(w + ": level " + std::to_string(l) +
+                                " needs an output and a nonzero tile shape");
+        if (lat) {
+            // every tile of every frame inside the lattice buffer: a bad
+            // offset must be an argument error here, not a device fault
+            const aqz_chunk_lattice& c = lat[l];
+            const uint64_t ntiles = uint64_t((ds->lv[l].width + tc - 1) / tc) *
+                                    ((ds->lv[l].height + tr - 1) / tr);
+            const uint64_t tile_bytes = uint64_t(tr) * tc * ds->bpp;
+            if (!c.frame_offset_bytes || c.chunk_stride_bytes % ds->bpp ||
+                c.chunk_stride_bytes < tile_bytes)
+                return ds->fail_arg(w + ": level " + std::to_string(l) +
+                                    ": chunk stride must hold a tile and be a multiple of the "
+                                    "pixel size, and frame offsets are required");
+            const uint64_t extent = (ntiles - 1) * c.chunk_stride_bytes + tile_bytes;
+            for (uint32_t k = 0; k < n_frames; ++k) {
+                const uint64_t off = c.frame_offset_bytes[k];
+                if (off % ds->bpp || off > c.capacity_bytes || c.capacity_bytes - off < extent)
+                    return ds->fail_arg(w + ": level " + std::to_string(l) + " frame " +
+                                        std::to_string(k) + ": offset " + std::to_string(off) +
+                                        " puts its tiles outside the lattice buffer");
+            }
+        }
+    }
+    if (int rc = bind_device(ds))
+        return rc;
+    hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ds->stream;
+    std::vector<const uint64_t*> d_off;
+    int half = -1;
+    if (lat)
+        if (int rc = stage_lattice(ds, lat, n_frames, stream, &d_off, &half))
+            return rc;
+
+    // Runs of up to kMaxFusedLevels levels; a run that feeds another also
+    // writes its last level row-major into one half of d_chain (the runs
+    // alternate halves, so a run never reads the half it writes).  The
+    // first chained level is the largest: 1/256 of the base after 4 levels.
+    const uint32_t first_feed = aqz::kMaxFusedLevels;
+    if (first_feed + 1 < ds->n) {
+        const size_t chain_half = size_t(n_frames) * ds->bytes[first_feed];
+        if (ds->d_chain_bytes < 2 * chain_half) {
+            HIP_TRY(ds, hipStreamSynchronize(stream), "hipStreamSynchronize");
+            (void)hipFree(ds->d_chain);
+            ds->d_chain = nullptr;
+            ds->d_chain_bytes = 0;
+            HIP_TRY(ds, hipMalloc(&ds->d_chain, 2 * chain_half), "hipMalloc chain");
+            ds->d_chain_bytes = 2 * chain_half;
+        }
+    }
+    const void* src = device_frames;
+    for (uint32_t L = 1, run = 0; L < ds->n; ++run) {
+        const uint32_t k = std::min<uint32_t>(ds->n - L, aqz::kMaxFusedLevels);
+        const bool feeds = L + k < ds->n;
+        aqz::LevelOut o[aqz::kMaxFusedLevels];
+        aqz::TiledOut t[aqz::kMaxFusedLevels];
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t l = L + j;
+            o[j] = { nullptr, elems(ds, l), ds->lv[l].width, ds->lv[l].height };
+            uint8_t* nz = device_tile_nonzero ? device_tile_nonzero[l] : nullptr;
+            if (lat)
+                t[j] = { lat[l].device_base, lat[l].tile_rows, lat[l].tile_cols, nz, d_off[l],
+                         lat[l].chunk_stride_bytes / ds->bpp };
+            else
+                t[j] = { device_out_levels[l], tile_rows[l], tile_cols[l], nz };
+        }
+        void* chain = static_cast<uint8_t*>(ds->d_chain) + (run & 1) * (ds->d_chain_bytes / 2);
+        if (feeds)
+            o[k - 1].ptr = chain;
+        const aqz_level_desc& a = ds->lv[L - 1];
+        if (!aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width, a.height, o,
+                                    int(k)))
+            return ds->fail_arg(w + ": level " + std::to_string(L - 1) +
+                                " is narrower than one vector load (" + std::to_string(a.width) +
+                                " px)");
+        const hipError_t e = aqz::launch_cascade_tiled(ds->dtype, ds->method, src,
+                                                       elems(ds, L - 1), a.width, a.height, o, t,
+                                                       int(k), n_frames, stream);
+        if (e != hipSuccess)
+            return e == hipErrorInvalidValue ? ds->fail_arg(w + ": unsupported geometry")
+                                             : ds->fail(e, "batch tiled cascade");
+        src = chain;
+        L += k;
+    }
+    if (lat)
+        HIP_TRY(ds, hipEventRecord(ds->lattice_done[half], stream), "hipEventRecord lattice");
+    for (uint32_t l = 0; l < ds->n; ++l) {
+        ds->count[l] += n_frames;
+        if (out_counts)
+            out_counts[l] = n_frames;
+    }
+    ds->last_batch_kind = 4;
+    return AQZ_OK;
+}
+
+} // namespace
+
+extern "C" {
+
 int
 aqz_ds_run_device_batch_tiled(aqz_ds* ds,
                               const void* device_frames,
@@ -1511,81 +1786,30 @@ aqz_ds_run_device_batch_tiled(aqz_ds* ds,
     try {
         if (!ds)
             return AQZ_INVALID_ARGUMENT;
-        if (int rc = settle(ds))
-            return rc;
-        if (ds->transpose)
-            return ds->fail_arg("run_device_batch_tiled: input transposition applies to the "
-                                "per-frame path only");
-        ds->last_input = nullptr;
-        if (!device_frames || !device_out_levels || !tile_rows || !tile_cols)
-            return ds->fail_arg("run_device_batch_tiled: null argument");
-        if (ds->n < 2)
-            return ds->fail_arg("run_device_batch_tiled: the pyramid has no level to tile");
-        for (uint32_t l = 1; l < ds->n; ++l) {
-            if (!ds->xy[l] || ds->zh[l])
-                return ds->fail_arg("run_device_batch_tiled: pure-XY (2-D) pyramids only; "
-                                    "level " + std::to_string(l) + " does not halve XY alone");
-            if (!device_out_levels[l] || !tile_rows[l] || !tile_cols[l])
-                return ds->fail_arg("run_device_batch_tiled: level " + std::to_string(l) +
-                                    " needs an output and a nonzero tile shape");
-        }
-        if (int rc = bind_device(ds))
-            return rc;
-        hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ds->stream;
+        return run_tiled(ds, "run_device_batch_tiled", device_frames, n_frames, tile_rows,
+                         tile_cols, device_out_levels, nullptr, device_tile_nonzero, out_counts,
+                         hip_stream);
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
+}
 
-        // Runs of up to kMaxFusedLevels levels; a run that feeds another also
-        // writes its last level row-major into one half of d_chain (the runs
-        // alternate halves, so a run never reads the half it writes).  The
-        // first chained level is the largest: 1/256 of the base after 4 levels.
-        const uint32_t first_feed = aqz::kMaxFusedLevels;
-        if (first_feed + 1 < ds->n) {
-            const size_t half = size_t(n_frames) * ds->bytes[first_feed];
-            if (ds->d_chain_bytes < 2 * half) {
-                HIP_TRY(ds, hipStreamSynchronize(stream), "hipStreamSynchronize");
-                (void)hipFree(ds->d_chain);
-                ds->d_chain = nullptr;
-                ds->d_chain_bytes = 0;
-                HIP_TRY(ds, hipMalloc(&ds->d_chain, 2 * half), "hipMalloc chain");
-                ds->d_chain_bytes = 2 * half;
-            }
-        }
-        const void* src = device_frames;
-        for (uint32_t L = 1, run = 0; L < ds->n; ++run) {
-            const uint32_t k = std::min<uint32_t>(ds->n - L, aqz::kMaxFusedLevels);
-            const bool feeds = L + k < ds->n;
-            aqz::LevelOut o[aqz::kMaxFusedLevels];
-            aqz::TiledOut t[aqz::kMaxFusedLevels];
-            for (uint32_t j = 0; j < k; ++j) {
-                o[j] = { nullptr, elems(ds, L + j), ds->lv[L + j].width, ds->lv[L + j].height };
-                t[j] = { device_out_levels[L + j], tile_rows[L + j], tile_cols[L + j],
-                         device_tile_nonzero ? device_tile_nonzero[L + j] : nullptr };
-            }
-            void* chain = static_cast<uint8_t*>(ds->d_chain) + (run & 1) * (ds->d_chain_bytes / 2);
-            if (feeds)
-                o[k - 1].ptr = chain;
-            const aqz_level_desc& a = ds->lv[L - 1];
-            if (!aqz::cascade_supported(ds->dtype, src, elems(ds, L - 1), a.width, a.height, o,
-                                        int(k)))
-                return ds->fail_arg("run_device_batch_tiled: level " + std::to_string(L - 1) +
-                                    " is narrower than one vector load (" +
-                                    std::to_string(a.width) + " px)");
-            const hipError_t e =
-              aqz::launch_cascade_tiled(ds->dtype, ds->method, src, elems(ds, L - 1), a.width,
-                                        a.height, o, t, int(k), n_frames, stream);
-            if (e != hipSuccess)
-                return e == hipErrorInvalidValue
-                         ? ds->fail_arg("run_device_batch_tiled: unsupported geometry")
-                         : ds->fail(e, "batch tiled cascade");
-            src = chain;
-            L += k;
-        }
-        for (uint32_t l = 0; l < ds->n; ++l) {
-            ds->count[l] += n_frames;
-            if (out_counts)
-                out_counts[l] = n_frames;
-        }
-        ds->last_batch_kind = 4;
-        return AQZ_OK;
+int
+aqz_ds_run_device_batch_chunked(aqz_ds* ds,
+                                const void* device_frames,
+                                uint32_t n_frames,
+                                const aqz_chunk_lattice* lattices,
+                                uint8_t* const* device_tile_nonzero,
+                                uint32_t* out_counts,
+                                void* hip_stream)
+{
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        if (!lattices)
+            return ds->fail_arg("run_device_batch_chunked: null lattices");
+        return run_tiled(ds, "run_device_batch_chunked", device_frames, n_frames, nullptr,
+                         nullptr, nullptr, lattices, device_tile_nonzero, out_counts, hip_stream);
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
     }

@@ -387,6 +387,65 @@ uint32_t aqz_ds_tiled_flag_slots(const aqz_ds* ds,
                                  uint32_t tile_cols);
 
 /*
+ * One level's chunk lattice in device memory: the chunk buffers of
+ * Array::chunks_ (array.cpp:563-617), `chunk_stride_bytes` apart, so tile
+ * t of frame k lands in chunk t + tile_group_offset(k) at
+ * chunk_internal_offset(k) (array.dimensions.cpp:265-314).
+ * `frame_offset_bytes` (host, n_frames entries) gives, per frame of the
+ * batch, where its tile 0 goes: tile_group_offset * chunk_stride_bytes +
+ * chunk_internal_offset, plus the layer's base when the buffer holds several
+ * chunk layers (aqz_chunk_frame_offsets computes exactly that).
+ */
+typedef struct
+{
+    void* device_base;
+    size_t capacity_bytes;        /* bytes at device_base: every tile must fit */
+    uint32_t tile_rows, tile_cols; /* the level's XY chunk shape */
+    size_t chunk_stride_bytes;    /* >= one tile; usually bytes_per_chunk */
+    const uint64_t* frame_offset_bytes;
+} aqz_chunk_lattice;
+
+/*
+ * aqz_ds_run_device_batch_tiled with every tile written straight into its
+ * chunk buffer (SURVEY §8(f) row 2 up to whole chunks): `lattices[L]` per
+ * level (index 0 ignored); the tiles, zero overhang and zero-scan flags are
+ * those of the tiled batch (device_tile_nonzero as there: per frame, not per
+ * chunk).  A frame whose tiles would leave the lattice buffer, an offset or
+ * stride that is not a multiple of the pixel size, or a stride below one
+ * tile is AQZ_INVALID_ARGUMENT before anything runs.  The offsets cross to
+ * the device on `hip_stream` with the batch; the call returns without
+ * synchronising, and `lattices` may be freed on return.
+ */
+int aqz_ds_run_device_batch_chunked(aqz_ds* ds,
+                                    const void* device_frames,
+                                    uint32_t n_frames,
+                                    const aqz_chunk_lattice* lattices,
+                                    uint8_t* const* device_tile_nonzero,
+                                    uint32_t* out_counts,
+                                    void* hip_stream);
+
+/*
+ * Where frames first_frame .. first_frame + n_frames - 1 of an array with
+ * storage-order dimensions `dims` (ndims >= 3, the last two Y and X) put
+ * their tile 0 in a lattice of chunk buffers `*chunk_bytes` apart:
+ *   (layer(k) - layer(first_frame)) * *layer_bytes
+ *     + tile_group_offset(k) * *chunk_bytes + chunk_internal_offset(k)
+ * restating ArrayDimensions::chunk_lattice_index / tile_group_offset /
+ * chunk_internal_offset (array.dimensions.cpp:232-314); *chunk_bytes =
+ * bytes_per_chunk (every dim's chunk size x bytes_per_px), *layer_bytes =
+ * the chunks of one append-dimension chunk layer (the buffer Array::chunks_
+ * holds) x *chunk_bytes.  Frame ids are in storage order.
+ */
+int aqz_chunk_frame_offsets(const aqz_dimension* dims,
+                            uint32_t ndims,
+                            uint32_t bytes_per_px,
+                            uint64_t first_frame,
+                            uint32_t n_frames,
+                            uint64_t* frame_offset_bytes,
+                            uint64_t* chunk_bytes,
+                            uint64_t* layer_bytes);
+
+/*
  * Host-resident batch, pipelined (overlapping frames).
  * Same results as aqz_ds_add_frame + aqz_ds_take_frame(every level) on each
  * of `n_frames` consecutive frames of `host_frames`: the k-th frame emitted at

@@ -2,8 +2,9 @@
 256x256 u16 = 128 KiB): compress_in_place (zarr.common.cpp:106-137) per chunk.
 
   cblosc   : the image's c-blosc 1.21.0, blosc_compress_ctx(nthreads=1) per
-             chunk, chunks spread over T host threads (the reference runs one
-             compression job per chunk on its thread pool) — host-resident input;
+             chunk, chunks spread over T pthreads (oracle/blosc_cpu.c; the
+             reference runs one compression job per chunk on its thread
+             pool) — host-resident input, no Python in the loop;
   aqz      : aqz_blosc_compress_device on the device-resident chunks: GPU
              filter, grouped D2H of the filtered chunks, LZ4/zstd on T host
              threads — device-resident input (the chunks the tiled pyramid or
@@ -54,6 +55,15 @@ def main():
     stride = nb + 16
     dst = np.empty(a.chunks * stride, np.uint8)
     pool = ThreadPoolExecutor(a.threads)
+    import ctypes
+    cpu = ctypes.CDLL(os.path.join(ROOT, "oracle", "libblosc_cpu.so"))
+    cpu.cblosc_compress_chunks.restype = ctypes.c_double
+    cpu.cblosc_compress_chunks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
+    cdst = np.empty(a.chunks * (nb + 16), np.uint8)
+    csizes = (ctypes.c_size_t * a.chunks)()
     for cname, clevel, shuffle in (("lz4", 1, 1), ("lz4", 5, 2), ("zstd", 1, 1), ("zstd", 3, 2)):
         frames = ctx.compress_device(clevel, shuffle, 2, cname, d.data_ptr(), nb, a.chunks)
         ref = list(pool.map(lambda k: blosc_ref.compress(raw[k * nb:(k + 1) * nb], clevel,
@@ -61,16 +71,21 @@ def main():
         assert frames == ref, "frame mismatch"
         ratio = sum(map(len, ref)) / raw.size
 
-        def run_ref():
-            list(pool.map(lambda k: blosc_ref.compress(raw[k * nb:(k + 1) * nb], clevel,
-                                                       shuffle, 2, cname), range(a.chunks)))
-
         def run_aqz():
             ctx.compress_device(clevel, shuffle, 2, cname, d.data_ptr(), nb, a.chunks,
                                 host_dst=dst, dst_stride=stride)
 
         res = {}
-        for name, fn in (("cblosc", run_ref), ("aqz", run_aqz)):
+        res["cblosc"] = cpu.cblosc_compress_chunks(raw.ctypes.data, nb, a.chunks, clevel, shuffle,
+                                                   2, cname.encode(), a.threads, cdst.ctypes.data,
+                                                   nb + 16, csizes, a.reps)
+        assert res["cblosc"] > 0, res
+        assert [cdst[k * (nb + 16):k * (nb + 16) + csizes[k]].tobytes()
+                for k in range(a.chunks)] == ref
+        res["cblosc_1thread"] = cpu.cblosc_compress_chunks(
+            raw.ctypes.data, nb, a.chunks, clevel, shuffle, 2, cname.encode(), 1,
+            cdst.ctypes.data, nb + 16, csizes, 2)
+        for name, fn in (("aqz", run_aqz),):
             fn()
             ts = []
             for _ in range(a.reps):
@@ -82,6 +97,7 @@ def main():
                           "chunks": a.chunks, "chunk_bytes": nb, "threads": a.threads,
                           "ratio": round(ratio, 4),
                           "cblosc_ms": round(res["cblosc"] * 1e3, 3),
+                          "cblosc_1thread_ms": round(res["cblosc_1thread"] * 1e3, 3),
                           "aqz_ms": round(res["aqz"] * 1e3, 3),
                           "cblosc_GBps": round(raw.size / res["cblosc"] / 1e9, 2),
                           "aqz_GBps": round(raw.size / res["aqz"] / 1e9, 2),
