@@ -369,6 +369,7 @@ struct CascadeParams
     uint32_t zwaves;                 // zero-fill waves: the grid's first zwaves / 4 blocks
     uint32_t main_blocks;            // blocks of cascade waves after them
     uint32_t remap;                  // 1: XCD-contiguous block order (cascade_kernel)
+    uint32_t wb;                     // bit J-1: level J's row-major stores write-back, not nt
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
 };
 
@@ -404,6 +405,19 @@ tiled_zwaves_env()
 {
     static const int v = [] {
         const char* e = std::getenv("AQZ_TILED_ZWAVES");
+        return (e && *e) ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
+// $AQZ_STORE_WB: unset = the launcher's default, else a level bit mask
+// (bit J-1 = level J) of row-major stores issued write-back instead of
+// non-temporal (A/B).
+inline int
+store_wb_env()
+{
+    static const int v = [] {
+        const char* e = std::getenv("AQZ_STORE_WB");
         return (e && *e) ? std::atoi(e) : -1;
     }();
     return v;
@@ -852,6 +866,10 @@ cascade_level(const CascadeParams& p,
             store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
                                                     col0, row0, lane);
         }
+    } else if ((p.wb >> (J - 1)) & 1u) {
+        // write-back: partial 64-B bursts of neighbouring waves merge in L2
+        store_level<T, C, J, RO, CO, EDGE, false>(dst, out, p.w[J - 1], p.h[J - 1], col0, row0,
+                                                  lane);
     } else {
         store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
                                                 col0, row0, lane);
@@ -1739,6 +1757,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         const uint32_t grid = grid_for(total, 4, 0);
         p.main_blocks = grid;
         p.remap = xcd_remap_env() == 1;
+        p.wb = store_wb_env() >= 0 ? uint32_t(store_wb_env()) : 0u;
         p.nt = load_nt(W, sizeof(T));
         // Band staging when some level's rows are not whole 64-byte bursts
         // and a row band is at most 4 tiles ($AQZ_BAND_STAGING=0: never).
