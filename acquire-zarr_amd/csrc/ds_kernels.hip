@@ -370,6 +370,7 @@ struct CascadeParams
     uint32_t main_blocks;            // blocks of cascade waves after them
     uint32_t remap;                  // 1: XCD-contiguous block order (cascade_kernel)
     uint32_t wb;                     // bit J-1: level J's row-major stores write-back, not nt
+    uint32_t order;                  // unit order: 0 columns fastest, 1 frames, 2 row bands
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
 };
 
@@ -421,6 +422,16 @@ store_wb_env()
         return (e && *e) ? std::atoi(e) : -1;
     }();
     return v;
+}
+
+// $AQZ_UNIT_ORDER (0 columns fastest = default, 1 frames fastest, 2 row bands
+// fastest) and $AQZ_CASCADE_WAVES (waves per workgroup, 4 = default, up to
+// 8): A/B switches of the row-major cascade's unit-to-wave mapping.
+inline int
+int_env(const char* name, int dflt)
+{
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atoi(e) : dflt;
 }
 
 // $AQZ_XCD_REMAP: unset = the launcher's default, 0 = off, 1 = on (A/B only).
@@ -927,7 +938,7 @@ cascade_unit(const CascadeParams& p,
 // in chunk-tile order (store_level_tiled); the grid's first blocks zero-fill
 // the tile overhang its cascade blocks do not reach (zero_fill_tiled).
 template<typename T, int M, int NL, int C = kCascadeCols<T>, bool NT = true, int TILED = 0>
-__global__ __launch_bounds__(256) void
+__global__ __launch_bounds__(512) void
 cascade_kernel(CascadeParams p)
 {
     // one tile per wave, the grid covers every tile (no grid-stride loop:
@@ -960,10 +971,24 @@ cascade_kernel(CascadeParams p)
     const uint32_t u = blk * (blockDim.x >> 6) + wave;
     if (u >= p.total_units)
         return;
-    const uint32_t ux = u % p.units_x;
-    const uint32_t t = u / p.units_x;
-    const uint32_t uy = t % p.units_y;
-    const uint32_t f = t / p.units_y;
+    uint32_t ux, uy, f;
+    if (TILED || p.order == 0) {
+        ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        uy = t % p.units_y;
+        f = t / p.units_y;
+    } else if (p.order == 1) {
+        const uint32_t nf = p.total_units / (p.units_x * p.units_y);
+        f = u % nf;
+        const uint32_t t = u / nf;
+        ux = t % p.units_x;
+        uy = t / p.units_x;
+    } else {
+        uy = u % p.units_y;
+        const uint32_t t = u / p.units_y;
+        ux = t % p.units_x;
+        f = t / p.units_x;
+    }
     const uint32_t row0 = uy * R;
     const uint32_t tile_col0 = ux * (64u * C);
     const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
@@ -984,7 +1009,7 @@ cascade_kernel(CascadeParams p)
 // share bursts with the neighbouring bands.  Partial-burst writes measured
 // 30% slower than whole ones on MI355X (tools/pitchbench.hip).
 template<typename T, int M, int NL, int C>
-__global__ __launch_bounds__(256) void
+__global__ __launch_bounds__(512) void
 cascade_band_kernel(CascadeParams p, uint32_t stage_mask)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t band_lds[];
@@ -1754,8 +1779,11 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             p.h[i] = outs[i].h;
         }
         // 4 waves per block, one tile per wave per iteration.
-        const uint32_t grid = grid_for(total, 4, 0);
+        static const uint32_t wpb = uint32_t(std::clamp(int_env("AQZ_CASCADE_WAVES", 4), 1, 8));
+        static const uint32_t order = uint32_t(std::clamp(int_env("AQZ_UNIT_ORDER", 0), 0, 2));
+        const uint32_t grid = grid_for(total, wpb, 0);
         p.main_blocks = grid;
+        p.order = order;
         p.remap = xcd_remap_env() == 1;
         p.wb = store_wb_env() >= 0 ? uint32_t(store_wb_env()) : 0u;
         p.nt = load_nt(W, sizeof(T));
@@ -1777,10 +1805,32 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             const char* v = std::getenv("AQZ_BAND_STAGING");
             return v && std::strcmp(v, "0") == 0;
         }();
-        const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask);
+        // Aligned frames of 5-8 tiles per row band (the headline's 4096 u16
+        // pixels, 3072, 4096 f32) stage every level too, in 8-wave
+        // workgroups, so each level's band leaves as one contiguous span.
+        // On most MI355X boxes tried, row-major level rows at a >= 4 KiB
+        // pitch written 512 B per wave ran 15-20% below the same kernel with
+        // tile-order stores; staged bands remove that (headline 535 -> 463
+        // us, 3072^2 541 -> 448 us; profiles/r02/band8_*).  Misaligned
+        // bands that wide stay direct: staging them cost 27% at 3000^2.
+        // $AQZ_BAND_ALIGNED=0 turns this off; $AQZ_BAND_FORCE (A/B) stages a
+        // level mask whatever the alignment, in bands of up to 8 waves.
+        static const uint32_t band_force = uint32_t(int_env("AQZ_BAND_FORCE", 0));
+        static const bool band_aligned = int_env("AQZ_BAND_ALIGNED", 1) != 0;
         const uint32_t band_waves = p.units_x;
+        const uint32_t all_levels = (1u << n_out) - 1u;
+        uint32_t wide_max = 4;
+        if (band_force) {
+            stage_mask |= band_force & all_levels;
+            wide_max = 8;
+        } else if (band_aligned && stage_mask == 0 && band_waves >= 5 && band_waves <= 8 &&
+                   band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= 65536) {
+            stage_mask = all_levels;
+            wide_max = 8;
+        }
+        const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask);
         const bool band = stage_mask && !band_off &&
-                          band_waves <= 4 && lds <= 65536 &&
+                          band_waves <= wide_max && lds <= 65536 &&
                           total < (1ull << 31);
         const uint32_t bands = p.units_y * n_frames;
         return with_method(method, [&](auto mtag) -> hipError_t {
@@ -1812,19 +1862,19 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                 }
                 switch (n_out) {
                     case 1:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT>), dim3(grid), dim3(64 * wpb),
                                            0, stream, p);
                         break;
                     case 2:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT>), dim3(grid), dim3(64 * wpb),
                                            0, stream, p);
                         break;
                     case 3:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT>), dim3(grid), dim3(64 * wpb),
                                            0, stream, p);
                         break;
                     default:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT>), dim3(grid), dim3(256),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT>), dim3(grid), dim3(64 * wpb),
                                            0, stream, p);
                         break;
                 }

@@ -433,7 +433,8 @@ def main():
     cpu_baseline = None
     e2e = None
     if rank == 0 and world == 1 and not args.no_pmc:
-        traffic = measure_traffic(args, "volume_kernel" if Z else "cascade_kernel")
+        # cascade_kernel or cascade_band_kernel (row bands staged in LDS)
+        traffic = measure_traffic(args, "volume_kernel" if Z else "cascade_")
         if traffic is not None:
             roofline["traffic"] = traffic["bytes_per_launch"]
             roofline["traffic_detail"] = traffic
@@ -453,6 +454,8 @@ def main():
                                                      d_in, min(B, 64), device)
             e2e["secondary_kernels"] = measure_secondary(aqz, torch, stream, d_in, W, H,
                                                          dtype, chunk)
+            # §8(f) row 3 end to end: c-blosc frames of device chunks vs c-blosc
+            e2e["blosc_frames"] = measure_blosc_frames(aqz, torch)
             if args.sink:
                 e2e["filesystem_sink"] = measure_e2e_sink(aqz, geo, dtype, method,
                                                           args.e2e_frames, device,
@@ -616,6 +619,63 @@ def measure_secondary(aqz, torch, stream, d_in, W, H, dtype, chunk, reps=20):
     orc_mod.transpose_frame(frame)
     res["transpose_kernel"]["cpu_reference_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
     return res
+
+
+def measure_blosc_frames(aqz, torch, threads=16, n_chunks=256, reps=5):
+    """compress_in_place (zarr.common.cpp:106-137) on one headline frame's
+    level-0 chunks (256 x 256x256 u16; smooth synthetic image + noise, since
+    the uniform bench input is incompressible): aqz_blosc_compress_device
+    from device-resident chunks against c-blosc itself on `threads` C
+    threads from host-resident chunks (oracle/libblosc_cpu.so, the CPU leg),
+    lz4 clevel 1 with byte shuffle.  Frames are checked byte-identical."""
+    import ctypes
+    import blosc_ref  # checker / CPU leg only
+    if not blosc_ref.available():
+        return None
+    rng = np.random.default_rng(5)
+    yy, xx = np.mgrid[0:256, 0:256]
+    host = np.empty((n_chunks, 256, 256), np.uint16)
+    for k in range(n_chunks):
+        host[k] = (2000 + 500 * np.sin((xx + 13 * k) / 17.0) * np.cos((yy - 5 * k) / 23.0)
+                   + rng.normal(0, 4, (256, 256))).astype(np.uint16)
+    raw = host.view(np.uint8).reshape(-1)
+    nb = 256 * 256 * 2
+    stride = nb + aqz.BLOSC_MAX_OVERHEAD
+    d = torch.from_numpy(raw.copy()).to("cuda")
+    torch.cuda.synchronize()
+    ctx = aqz.BloscContext(torch.cuda.current_device(), threads)
+    dst = np.empty(n_chunks * stride, np.uint8)
+    sizes = ctx.compress_device(1, aqz.SHUFFLE, 2, "lz4", d.data_ptr(), nb, n_chunks,
+                                host_dst=dst, dst_stride=stride)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.compress_device(1, aqz.SHUFFLE, 2, "lz4", d.data_ptr(), nb, n_chunks,
+                            host_dst=dst, dst_stride=stride)
+        ts.append(time.perf_counter() - t0)
+    ctx.close()
+    cpu = ctypes.CDLL(os.path.join(ROOT, "oracle", "libblosc_cpu.so"))
+    cpu.cblosc_compress_chunks.restype = ctypes.c_double
+    cpu.cblosc_compress_chunks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
+    cdst = np.empty(n_chunks * stride, np.uint8)
+    csz = (ctypes.c_size_t * n_chunks)()
+    t16 = cpu.cblosc_compress_chunks(raw.ctypes.data, nb, n_chunks, 1, 1, 2, b"lz4", threads,
+                                     cdst.ctypes.data, stride, csz, reps)
+    t1 = cpu.cblosc_compress_chunks(raw.ctypes.data, nb, n_chunks, 1, 1, 2, b"lz4", 1,
+                                    cdst.ctypes.data, stride, csz, 1)
+    same = all(sizes[k] == csz[k] and np.array_equal(dst[k * stride:k * stride + sizes[k]],
+                                                     cdst[k * stride:k * stride + csz[k]])
+               for k in range(n_chunks))
+    return {"chunks": n_chunks, "chunk_bytes": nb, "codec": "lz4 clevel 1 shuffle",
+            "ratio": round(sum(sizes) / raw.size, 4), "threads": threads,
+            "aqz_device_chunks_ms": round(min(ts) * 1e3, 3),
+            "cblosc_host_chunks_ms": round(t16 * 1e3, 3),
+            "cblosc_1thread_ms": round(t1 * 1e3, 3),
+            "frames_identical_to_cblosc": bool(same),
+            "cblosc_version": blosc_ref.version()}
 
 
 def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
