@@ -1070,6 +1070,26 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask)
     }
 }
 
+// LDS a band workgroup may use: the device's per-workgroup maximum (160 KiB
+// on gfx950, so f32 bands of 8 waves, 85 KiB, fit), 64 KiB if the query
+// fails; $AQZ_BAND_LDS_CAP (bytes) lowers it for A/B.
+inline uint32_t
+band_lds_cap()
+{
+    static const uint32_t cap = [] {
+        int dev = 0, v = 0;
+        uint32_t c = 65536;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) ==
+              hipSuccess &&
+            v > 0)
+            c = uint32_t(v);
+        const int e = int_env("AQZ_BAND_LDS_CAP", 0);
+        return e > 0 ? std::min(c, uint32_t(e)) : c;
+    }();
+    return cap;
+}
+
 // Bytes of LDS cascade_band_kernel needs for a band (upper bound over
 // bands; 0 if no level is staged).
 inline uint32_t
@@ -1824,13 +1844,13 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             stage_mask |= band_force & all_levels;
             wide_max = 8;
         } else if (band_aligned && stage_mask == 0 && band_waves >= 5 && band_waves <= 8 &&
-                   band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= 65536) {
+                   band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
             stage_mask = all_levels;
             wide_max = 8;
         }
         const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask);
         const bool band = stage_mask && !band_off &&
-                          band_waves <= wide_max && lds <= 65536 &&
+                          band_waves <= wide_max && lds <= band_lds_cap() &&
                           total < (1ull << 31);
         const uint32_t bands = p.units_y * n_frames;
         return with_method(method, [&](auto mtag) -> hipError_t {
@@ -1842,18 +1862,34 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                     const dim3 blk(64 * band_waves);
                     switch (n_out) {
                         case 1:
+                            if (lds > 65536) // above the default per-workgroup LDS
+                                (void)hipFuncSetAttribute(
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C>), dim3(bands), blk,
                                                lds, stream, p, stage_mask);
                             break;
                         case 2:
+                            if (lds > 65536) // above the default per-workgroup LDS
+                                (void)hipFuncSetAttribute(
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C>), dim3(bands), blk,
                                                lds, stream, p, stage_mask);
                             break;
                         case 3:
+                            if (lds > 65536) // above the default per-workgroup LDS
+                                (void)hipFuncSetAttribute(
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C>), dim3(bands), blk,
                                                lds, stream, p, stage_mask);
                             break;
                         default:
+                            if (lds > 65536) // above the default per-workgroup LDS
+                                (void)hipFuncSetAttribute(
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C>), dim3(bands), blk,
                                                lds, stream, p, stage_mask);
                             break;
