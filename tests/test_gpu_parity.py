@@ -184,6 +184,10 @@ BATCH_GEOMETRIES = {
     # is <= 4 tiles (u8 here), direct stores for wider bands (u16, f32, i64)
     "2d_wide_misaligned": (halving_geometry(2600, 70, 4), 3, 1),
     "2d_band_staged": (halving_geometry(1500, 90, 4), 3, 1),
+    # aligned row bands of 5-8 tiles: every level staged by 8-wave (u16, f32
+    # with 85 KiB of LDS) or 6-wave workgroups; u8 / i64 keep direct stores
+    "2d_band8_aligned": (halving_geometry(4096, 48, 4), 3, 1),
+    "2d_band6_edge_rows": (halving_geometry(3072, 37, 4), 3, 1),
 }
 
 
