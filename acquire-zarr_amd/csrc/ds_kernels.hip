@@ -804,6 +804,10 @@ struct StageCtx
     uint8_t* lds[kMaxFusedLevels];
     uint32_t head[kMaxFusedLevels];
     uint32_t mask; // bit J-1: level J is staged
+    // LDS row stride (elements) and first staged column per level: the
+    // level width and 0 for a whole band, the segment's for a segmented one
+    uint32_t stride[kMaxFusedLevels];
+    uint32_t scol[kMaxFusedLevels];
 };
 
 template<typename T, int C, int J, int RO, int CO, bool EDGE>
@@ -830,7 +834,8 @@ stage_level(const StageCtx& sc,
         }
         if (!ok)
             continue;
-        T* d = reinterpret_cast<T*>(base) + uint64_t(rout0 + r - (band_row0 >> J)) * wout + cout0;
+        T* d = reinterpret_cast<T*>(base) +
+               uint64_t(rout0 + r - (band_row0 >> J)) * sc.stride[J - 1] + (cout0 - sc.scol[J - 1]);
 #pragma unroll
         for (int c = 0; c < CO; ++c) {
             if (!EDGE || cout0 + c < wout)
@@ -1000,30 +1005,42 @@ cascade_kernel(CascadeParams p)
     }
 }
 
-// Band-staged cascade for frames whose level rows split 64-byte bursts
-// (widths like 2000 or 3000 px): one workgroup per row band of one frame,
-// one wave per column tile (blockDim = 64 * units_x, units_x <= 4).  Staged levels
-// (StageCtx) go to LDS; after one barrier the workgroup writes each staged
-// level's band — consecutive level rows are adjacent in memory — as one span
-// of whole, 16-byte-aligned chunks, so only the span's first and last chunk
-// share bursts with the neighbouring bands.  Partial-burst writes measured
-// 30% slower than whole ones on MI355X (tools/pitchbench.hip).
+// Band-staged cascade: one workgroup per row band of one frame, one wave per
+// column tile.  Staged levels (StageCtx) go to LDS; after one barrier the
+// workgroup writes each staged level's band — consecutive level rows are
+// adjacent in memory — as one span of whole, 16-byte-aligned chunks, so only
+// the span's first and last chunk share bursts with the neighbouring bands.
+// Used for frames whose level rows split 64-byte bursts (widths like 2000 or
+// 3000 px, bands of <= 4 tiles: partial-burst writes measured 30% slower
+// than whole ones, tools/pitchbench.hip) and for aligned bands of 5-8 tiles
+// (row-major rows at >= 4 KiB pitch written 512 B per wave ran 15% slow on
+// most boxes).  seg_tiles > 0 (aligned frames only): a band wider than that
+// is split into segments of seg_tiles tiles, one workgroup each, every level
+// row of a segment one contiguous piece; waves past the last tile only join
+// the barrier.
 template<typename T, int M, int NL, int C>
 __global__ __launch_bounds__(512) void
-cascade_band_kernel(CascadeParams p, uint32_t stage_mask)
+cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t band_lds[];
     constexpr int R = 1 << NL;
     const int lane = threadIdx.x & 63;
-    const uint32_t ux = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t uy = blockIdx.x % p.units_y;
-    const uint32_t f = blockIdx.x / p.units_y;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t segs = seg_tiles ? (p.units_x + seg_tiles - 1) / seg_tiles : 1u;
+    const uint32_t seg = blockIdx.x % segs;
+    const uint32_t band = blockIdx.x / segs;
+    const uint32_t uy = band % p.units_y;
+    const uint32_t f = band / p.units_y;
     const uint32_t row0 = uy * R;
+    const uint32_t ux = seg * seg_tiles + wave;
+    const uint32_t seg_col0 = seg * seg_tiles * 64u * C; // level-0 column
 
     // LDS regions of the staged levels (same arithmetic in every thread)
     StageCtx sc{};
     sc.mask = stage_mask;
-    uint32_t len[kMaxFusedLevels] = {};
+    uint32_t len[kMaxFusedLevels] = {};  // bytes per level row piece x rows
+    uint32_t rows_of[kMaxFusedLevels] = {};
+    uint32_t piece[kMaxFusedLevels] = {}; // bytes of one row's piece (segmented)
     uint8_t* span[kMaxFusedLevels] = {};
     uint32_t off = 0;
 #pragma unroll
@@ -1032,26 +1049,56 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask)
             continue;
         const uint32_t r0 = row0 >> (i + 1);
         const uint32_t rows = min(uint32_t(R >> (i + 1)), p.h[i] - min(r0, p.h[i]));
-        span[i] = p.dst[i] + (uint64_t(f) * p.dst_frame_elems[i] + uint64_t(r0) * p.w[i]) *
-                               sizeof(T);
-        len[i] = rows * p.w[i] * uint32_t(sizeof(T));
-        sc.head[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 15u);
+        rows_of[i] = rows;
+        if (seg_tiles) {
+            const uint32_t c0 = seg_col0 >> (i + 1);
+            const uint32_t cw = min((seg_tiles * 64u * C) >> (i + 1), p.w[i] - min(c0, p.w[i]));
+            sc.stride[i] = cw;
+            sc.scol[i] = c0;
+            piece[i] = cw * uint32_t(sizeof(T));
+            span[i] = p.dst[i] +
+                      (uint64_t(f) * p.dst_frame_elems[i] + uint64_t(r0) * p.w[i] + c0) * sizeof(T);
+            len[i] = rows * piece[i];
+            sc.head[i] = 0; // aligned frames: every piece starts on 16 bytes
+        } else {
+            sc.stride[i] = p.w[i];
+            sc.scol[i] = 0;
+            span[i] = p.dst[i] + (uint64_t(f) * p.dst_frame_elems[i] + uint64_t(r0) * p.w[i]) *
+                                   sizeof(T);
+            len[i] = rows * p.w[i] * uint32_t(sizeof(T));
+            sc.head[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 15u);
+        }
         sc.lds[i] = band_lds + off;
         off += (sc.head[i] + len[i] + 15u) & ~15u;
     }
 
-    const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
-    const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
-    if (interior)
-        cascade_unit<T, M, NL, C, true, false, true, true>(p, f, row0, col0, lane, &sc);
-    else
-        cascade_unit<T, M, NL, C, true, true, true, true>(p, f, row0, col0, lane, &sc);
+    if (ux < p.units_x) { // wave-uniform
+        const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
+        const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
+        if (interior)
+            cascade_unit<T, M, NL, C, true, false, true, true>(p, f, row0, col0, lane, &sc);
+        else
+            cascade_unit<T, M, NL, C, true, true, true, true>(p, f, row0, col0, lane, &sc);
+    }
     __syncthreads();
 
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
         if (!((stage_mask >> i) & 1u) || len[i] == 0)
             continue;
+        if (seg_tiles) {
+            // rows_of[i] pieces of piece[i] bytes, level pitch apart
+            const uint32_t cpr = piece[i] / 16u;
+            const uint32_t chunks = rows_of[i] * cpr;
+            const uint64_t pitch = uint64_t(p.w[i]) * sizeof(T);
+            for (uint32_t k = threadIdx.x; k < chunks; k += blockDim.x) {
+                const uint32_t r = k / cpr, c = k - r * cpr;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(sc.lds[i] + r * piece[i] + c * 16u);
+                __builtin_nontemporal_store(
+                  v, reinterpret_cast<u32x4*>(span[i] + r * pitch + c * 16u));
+            }
+            continue;
+        }
         const uint32_t head = sc.head[i];
         const uint32_t end = head + len[i];
         const uint32_t chunks = (end + 15u) / 16u;
@@ -1093,13 +1140,16 @@ band_lds_cap()
 // Bytes of LDS cascade_band_kernel needs for a band (upper bound over
 // bands; 0 if no level is staged).
 inline uint32_t
-band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask)
+band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
+               uint32_t seg_cols = 0)
 {
     uint64_t total = 0;
     for (int i = 0; i < n_out; ++i) {
         if ((stage_mask >> i) & 1u) {
             const uint64_t rows = uint64_t(1) << (n_out - i - 1);
-            total += (15 + rows * outs[i].w * b + 15) & ~uint64_t(15);
+            const uint64_t w = seg_cols ? std::min<uint64_t>(seg_cols >> (i + 1), outs[i].w)
+                                        : outs[i].w;
+            total += (15 + rows * w * b + 15) & ~uint64_t(15);
         }
     }
     return total > (1u << 30) ? (1u << 30) : uint32_t(total);
@@ -1835,11 +1885,17 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // bands that wide stay direct: staging them cost 27% at 3000^2.
         // $AQZ_BAND_ALIGNED=0 turns this off; $AQZ_BAND_FORCE (A/B) stages a
         // level mask whatever the alignment, in bands of up to 8 waves.
+        // Aligned bands wider than 8 tiles go in 8-tile segments, one
+        // workgroup each, every level row of a segment one contiguous piece:
+        // 8192x2048 u16 517 -> 485 us, 8704x2040 532 -> 447 us, 6144x3072
+        // 531 -> 516 us, 8192x2048 f32 1012 -> 962 us
+        // (profiles/r02/band8/segments_ab.log); $AQZ_BAND_SEGMENTS=0: off.
         static const uint32_t band_force = uint32_t(int_env("AQZ_BAND_FORCE", 0));
         static const bool band_aligned = int_env("AQZ_BAND_ALIGNED", 1) != 0;
-        const uint32_t band_waves = p.units_x;
+        static const bool band_segments = int_env("AQZ_BAND_SEGMENTS", 1) != 0;
+        uint32_t band_waves = p.units_x;
         const uint32_t all_levels = (1u << n_out) - 1u;
-        uint32_t wide_max = 4;
+        uint32_t wide_max = 4, seg_tiles = 0;
         if (band_force) {
             stage_mask |= band_force & all_levels;
             wide_max = 8;
@@ -1847,12 +1903,21 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
             stage_mask = all_levels;
             wide_max = 8;
+        } else if (band_aligned && band_segments && stage_mask == 0 && band_waves > 8 &&
+                   band_lds_bytes(sizeof(T), outs, n_out, all_levels, 8u * 64u * cols) <=
+                     band_lds_cap()) {
+            stage_mask = all_levels;
+            seg_tiles = 8;
+            band_waves = 8;
+            wide_max = 8;
         }
-        const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask);
+        const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask,
+                                            seg_tiles * 64u * cols);
         const bool band = stage_mask && !band_off &&
                           band_waves <= wide_max && lds <= band_lds_cap() &&
                           total < (1ull << 31);
-        const uint32_t bands = p.units_y * n_frames;
+        const uint32_t segs = seg_tiles ? (p.units_x + seg_tiles - 1) / seg_tiles : 1u;
+        const uint32_t bands = p.units_y * n_frames * segs;
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
             auto go = [&](auto ctag, auto nttag) {
@@ -1867,7 +1932,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask);
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                         case 2:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -1875,7 +1940,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask);
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                         case 3:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -1883,7 +1948,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask);
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                         default:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -1891,7 +1956,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask);
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                     }
                     return;

@@ -188,6 +188,9 @@ BATCH_GEOMETRIES = {
     # with 85 KiB of LDS) or 6-wave workgroups; u8 / i64 keep direct stores
     "2d_band8_aligned": (halving_geometry(4096, 48, 4), 3, 1),
     "2d_band6_edge_rows": (halving_geometry(3072, 37, 4), 3, 1),
+    # aligned bands wider than 8 tiles: 8-tile segments (u8 9 tiles, u16 /
+    # f32 17, i64 34), a last segment of one or two tiles, odd band rows
+    "2d_band_segments": (halving_geometry(8704, 40, 4), 2, 1),
 }
 
 
