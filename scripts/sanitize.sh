@@ -2,7 +2,8 @@
 # Host-code sanitizers (GPU ASan is not available on this pool):
 #  1. the C oracle under ASan+UBSan (gcc), driven by tests/sanitize/oracle_fuzz.c
 #  2. the product library's host code under ASan+UBSan (hipcc -Xarch_host),
-#     driven by tests/sanitize/abi_host.c (planner, validation, strings).
+#     driven by tests/sanitize/abi_host.c (planner, validation, strings,
+#     chunk-lattice offsets, the blosc frame writer with real LZ4/zstd).
 set -eu
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 OUT="${TMPDIR:-/tmp}/aqz_sanitize"
@@ -22,13 +23,15 @@ for k in 0 1 2 3 4 5 6 7; do
       -o "$OUT/ds_kernels_s$k.o" &
   pids+=($!)
 done
-for f in ds_dispatch.cpp ds_runtime.cpp; do
+for f in ds_dispatch.cpp ds_runtime.cpp codec_runtime.cpp blosc_frame.cpp; do
   $HIPCC $HF $HS -DAQZ_SHARDS=8 -x hip -c "$ROOT/acquire-zarr_amd/csrc/$f" -o "$OUT/${f%.*}.o"
 done
+$HIPCC $HF $HS -c "$ROOT/acquire-zarr_amd/csrc/codec_kernels.hip" -o "$OUT/codec_kernels.o"
 for p in "${pids[@]}"; do wait "$p"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC -fsanitize=address,undefined \
-    "$OUT"/ds_kernels_s?.o "$OUT/ds_dispatch.o" "$OUT/ds_runtime.o" -o "$OUT/libaqz_san.so" \
-    -Wl,-rpath,/opt/rocm/lib
+    "$OUT"/ds_kernels_s?.o "$OUT/ds_dispatch.o" "$OUT/ds_runtime.o" "$OUT/codec_runtime.o" \
+    "$OUT/codec_kernels.o" "$OUT/blosc_frame.o" -o "$OUT/libaqz_san.so" \
+    -Wl,-rpath,/opt/rocm/lib -ldl -lpthread
 # the driver must use the same (clang) sanitizer runtime as the library
 /opt/rocm/lib/llvm/bin/clang -g -fsanitize=address,undefined -I"$ROOT/include" \
     "$ROOT/tests/sanitize/abi_host.c" "$OUT/libaqz_san.so" \

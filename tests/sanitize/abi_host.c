@@ -2,9 +2,11 @@
  * (planner, argument validation, method strings) — no GPU needed.
  * Built and run by scripts/sanitize.sh against a host-sanitized build of
  * libaqz_downsampler. */
+#include "aqz_blosc.h"
 #include "aqz_downsampler.h"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 int
@@ -58,6 +60,52 @@ main(void)
     if (aqz_ds_run_device_batch(NULL, NULL, 1, outs, NULL, NULL) != AQZ_INVALID_ARGUMENT)
         return 14;
     aqz_ds_destroy(NULL);
-    printf("abi_host: ok (%s)\n", aqz_version());
+    if (aqz_ds_run_device_batch_chunked(NULL, NULL, 1, NULL, NULL, NULL, NULL) !=
+        AQZ_INVALID_ARGUMENT)
+        return 15;
+    /* chunk-lattice offsets (T/C/Y/X, ragged chunks) */
+    aqz_dimension nd[4] = { { AQZ_DIM_TIME, 0, 2, 1, 1.0 },
+                            { AQZ_DIM_CHANNEL, 3, 2, 1, 1.0 },
+                            { AQZ_DIM_SPACE, 100, 32, 1, 1.0 },
+                            { AQZ_DIM_SPACE, 90, 64, 1, 1.0 } };
+    uint64_t offs[37], cb = 0, lb = 0;
+    if (aqz_chunk_frame_offsets(nd, 4, 2, 5, 37, offs, &cb, &lb) ||
+        cb != 2ull * 2 * 2 * 32 * 64 || lb != 2 * 4 * 2 * cb)
+        return 16;
+    if (aqz_chunk_frame_offsets(nd, 2, 2, 0, 1, offs, &cb, &lb) != AQZ_INVALID_ARGUMENT)
+        return 17;
+    /* blosc frames from host-filtered blocks: every destination size from
+     * too small to roomy, compressible and incompressible chunks, both codecs;
+     * with byte shuffle off the "filtered" bytes are the chunk itself */
+    const size_t nb = 70001;
+    uint8_t* src = (uint8_t*)malloc(nb);
+    uint32_t x = 1;
+    for (size_t i = 0; i < nb; ++i) {
+        x = x * 1664525u + 1013904223u;
+        src[i] = (uint8_t)(i < nb / 2 ? (i / 97) & 7 : x >> 24);
+    }
+    const char* codecs[2] = { "lz4", "zstd" };
+    for (int c = 0; c < 2; ++c)
+        for (int clevel = 0; clevel <= 9; clevel += 3)
+            for (size_t dsz = 10; dsz < nb + 200; dsz += 7001) {
+                uint8_t* dst = (uint8_t*)malloc(dsz);
+                size_t fb = 0;
+                int raw = 0;
+                uint32_t bs = 0;
+                if (aqz_blosc_blocksize(clevel, 1, nb, codecs[c], &bs) || bs == 0)
+                    return 18;
+                if (aqz_blosc_frame_from_filtered(clevel, 0, 1, codecs[c], src, src, nb, dst,
+                                                  dsz, &fb, &raw))
+                    return 19;
+                if (fb > dsz)
+                    return 20;
+                free(dst);
+            }
+    uint32_t bs = 0;
+    if (aqz_blosc_blocksize(10, 2, nb, "lz4", &bs) != AQZ_INVALID_ARGUMENT ||
+        aqz_blosc_blocksize(5, 2, nb, "blosclz", &bs) != AQZ_INVALID_ARGUMENT)
+        return 21;
+    free(src);
+    printf("abi_host: ok (%s; %s)\n", aqz_version(), aqz_blosc_codec_info());
     return 0;
 }
