@@ -1018,7 +1018,7 @@ cascade_kernel(CascadeParams p)
 // is split into segments of seg_tiles tiles, one workgroup each, every level
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
-template<typename T, int M, int NL, int C>
+template<typename T, int M, int NL, int C, bool NT = true>
 __global__ __launch_bounds__(512) void
 cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
 {
@@ -1076,9 +1076,9 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
         const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
         if (interior)
-            cascade_unit<T, M, NL, C, true, false, true, true>(p, f, row0, col0, lane, &sc);
+            cascade_unit<T, M, NL, C, NT, false, true, true>(p, f, row0, col0, lane, &sc);
         else
-            cascade_unit<T, M, NL, C, true, true, true, true>(p, f, row0, col0, lane, &sc);
+            cascade_unit<T, M, NL, C, NT, true, true, true>(p, f, row0, col0, lane, &sc);
     }
     __syncthreads();
 
@@ -1929,33 +1929,33 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                         case 1:
                             if (lds > 65536) // above the default per-workgroup LDS
                                 (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C>),
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C>), dim3(bands), blk,
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C, NT>), dim3(bands), blk,
                                                lds, stream, p, stage_mask, seg_tiles);
                             break;
                         case 2:
                             if (lds > 65536) // above the default per-workgroup LDS
                                 (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C>),
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C>), dim3(bands), blk,
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C, NT>), dim3(bands), blk,
                                                lds, stream, p, stage_mask, seg_tiles);
                             break;
                         case 3:
                             if (lds > 65536) // above the default per-workgroup LDS
                                 (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C>),
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C>), dim3(bands), blk,
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C, NT>), dim3(bands), blk,
                                                lds, stream, p, stage_mask, seg_tiles);
                             break;
                         default:
                             if (lds > 65536) // above the default per-workgroup LDS
                                 (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C>),
+                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C>), dim3(bands), blk,
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C, NT>), dim3(bands), blk,
                                                lds, stream, p, stage_mask, seg_tiles);
                             break;
                     }
