@@ -540,6 +540,14 @@ aqz_blosc_compress_device(aqz_blosc_ctx* ctx, int clevel, int shuffle, uint32_t 
             BLOSC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
             ctx->events.push_back(e);
         }
+        // From the filter launch on, work that reads or writes ctx's scratch
+        // is queued on `stream`: every exit drains it first, so a failed call
+        // never leaves a copy into h_filtered in flight for the next one.
+        struct Drain
+        {
+            hipStream_t s;
+            ~Drain() { (void)hipStreamSynchronize(s); }
+        } drain{ stream };
         BLOSC_HIP(aqz::launch_blosc_filter(shuffle, p.typesize, static_cast<uint32_t>(bs), src,
                                            nbytes, n_buffers, ctx->d_filtered, stream),
                   "filter");

@@ -138,6 +138,9 @@ struct aqz_ds
     // fused run that feeds the next run (pyramids deeper than 4 XY levels)
     void* d_chain = nullptr;
     size_t d_chain_bytes = 0;
+    // recorded after every tiled batch: the next one (on any stream) waits on
+    // it before it rewrites d_chain
+    hipEvent_t chain_done = nullptr;
     // aqz_ds_run_device_batch_chunked: per-level frame offsets (elements),
     // staged in pinned memory and copied to the device on the batch's
     // stream; two halves used by alternate calls, each guarded by the event
@@ -663,6 +666,10 @@ release(aqz_ds* ds)
         }
     (void)hipFree(ds->d_lattice);
     (void)hipHostFree(ds->h_lattice);
+    if (ds->chain_done) {
+        (void)hipEventSynchronize(ds->chain_done);
+        (void)hipEventDestroy(ds->chain_done);
+    }
     (void)hipFree(ds->d_chain);
     for (auto& t : ds->tslot) {
         (void)hipFree(t.first);
@@ -1706,6 +1713,26 @@ run_tiled(aqz_ds* ds,
     if (lat)
         if (int rc = stage_lattice(ds, lat, n_frames, stream, &d_off, &half))
             return rc;
+    // From here on the staged half's upload is queued on `stream`: whatever
+    // the exit, record the event that guards the pinned half, so a later call
+    // never rewrites it while that copy may still read it.
+    struct LatticeGuard
+    {
+        aqz_ds* ds;
+        int half;
+        hipStream_t stream;
+        ~LatticeGuard()
+        {
+            if (half >= 0)
+                (void)hipEventRecord(ds->lattice_done[half], stream);
+        }
+    } lattice_guard{ ds, half, stream };
+    // A previous batch may still be reading or writing d_chain on another
+    // stream: order this one behind it.
+    if (ds->chain_done)
+        HIP_TRY(ds, hipStreamWaitEvent(stream, ds->chain_done, 0), "hipStreamWaitEvent chain");
+    else
+        HIP_TRY(ds, hipEventCreateWithFlags(&ds->chain_done, hipEventDisableTiming), "event");
 
     // Runs of up to kMaxFusedLevels levels; a run that feeds another also
     // writes its last level row-major into one half of d_chain (the runs
@@ -1757,8 +1784,7 @@ run_tiled(aqz_ds* ds,
         src = chain;
         L += k;
     }
-    if (lat)
-        HIP_TRY(ds, hipEventRecord(ds->lattice_done[half], stream), "hipEventRecord lattice");
+    HIP_TRY(ds, hipEventRecord(ds->chain_done, stream), "hipEventRecord chain");
     for (uint32_t l = 0; l < ds->n; ++l) {
         ds->count[l] += n_frames;
         if (out_counts)

@@ -73,7 +73,10 @@ int aqz_blosc_frame_from_filtered(int clevel,
                                   int* raw_needed);
 
 /* Device scratch, pinned staging and host worker threads for
- * aqz_blosc_compress_device.  n_threads 0: min(16, hardware threads). */
+ * aqz_blosc_compress_device.  n_threads 0: min(16, hardware threads).
+ * A ctx serves one call at a time: its scratch is shared by every call on
+ * it, so two threads must not use one ctx concurrently (one ctx per thread,
+ * as the reference's compression jobs would hold one each). */
 typedef struct aqz_blosc_ctx aqz_blosc_ctx;
 
 int aqz_blosc_ctx_create(int device, uint32_t n_threads, aqz_blosc_ctx** out);

@@ -363,7 +363,11 @@ int aqz_ds_run_device_batch(aqz_ds* ds,
  * Pure-XY (2-D) pyramids only, frames at least one 16-byte load wide, no
  * input transposition; anything else is AQZ_INVALID_ARGUMENT.  Runs on
  * `hip_stream` (NULL = the handle's stream) without synchronising;
- * `out_counts` as for aqz_ds_run_device_batch.
+ * `out_counts` as for aqz_ds_run_device_batch.  Pyramids deeper than 4
+ * levels chain runs through handle scratch, so each tiled/chunked batch is
+ * ordered behind the handle's previous one whatever stream either ran on
+ * (an event wait; no host synchronisation).  A handle is not thread-safe:
+ * one caller thread at a time, as for zarr::Downsampler.
  */
 int aqz_ds_run_device_batch_tiled(aqz_ds* ds,
                                   const void* device_frames,

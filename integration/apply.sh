@@ -14,4 +14,5 @@ patch -d "$tree" -p1 --forward --no-backup-if-mismatch < "$here/acquire-zarr-hip
 install -m 0644 "$here/cmake/hip.cmake" "$tree/cmake/hip.cmake"
 install -m 0644 "$here/src/streaming/downsampler.hip.cpp" "$tree/src/streaming/downsampler.hip.cpp"
 install -m 0644 "$here/src/streaming/array.tiled.cpp" "$tree/src/streaming/array.tiled.cpp"
+install -m 0644 "$here/src/streaming/array.tiled.hh" "$tree/src/streaming/array.tiled.hh"
 echo "acquire-zarr tree patched: configure with -DAQZ_DOWNSAMPLER=hip -DAQZ_DS_ROOT=$(dirname "$here")"

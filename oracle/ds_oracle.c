@@ -669,3 +669,101 @@ oracle_transpose_frame(int dtype,
     }
     return 0;
 }
+
+/* ---- chunk addressing (array.dimensions.cpp:232-314) -------------------- */
+
+/*
+ * ArrayDimensions::chunk_lattice_index (array.dimensions.cpp:232-262): the
+ * chunk index of frame `frame_id` along non-spatial dim `dim_index`.  Dim 0
+ * (the append dimension) divides by its chunk size times the array sizes of
+ * dims 1..ndims-3; the others take the frame id modulo the array sizes from
+ * dim_index on, divided by dim_index's chunk size times the faster sizes.
+ * Returns UINT32_MAX for a dim_index the reference's EXPECT rejects.
+ */
+uint32_t
+oracle_chunk_lattice_index(const oracle_dim* dims,
+                           uint32_t ndims,
+                           uint64_t frame_id,
+                           uint32_t dim_index)
+{
+    if (!dims || ndims < 3 || dim_index >= ndims - 2)
+        return UINT32_MAX;
+    if (dim_index == 0) {
+        uint64_t divisor = dims[0].chunk_size_px;
+        for (uint32_t i = 1; i < ndims - 2; ++i)
+            divisor *= dims[i].array_size_px;
+        return divisor ? (uint32_t)(frame_id / divisor) : UINT32_MAX;
+    }
+    uint64_t mod_divisor = 1, div_divisor = 1;
+    for (uint32_t i = dim_index; i < ndims - 2; ++i) {
+        mod_divisor *= dims[i].array_size_px;
+        div_divisor *=
+          i == dim_index ? dims[i].chunk_size_px : dims[i].array_size_px;
+    }
+    if (!mod_divisor || !div_divisor)
+        return UINT32_MAX;
+    return (uint32_t)((frame_id % mod_divisor) / div_divisor);
+}
+
+/*
+ * ArrayDimensions::tile_group_offset (array.dimensions.cpp:264-282): the
+ * index, in chunks, of the first chunk of the frame's tile group inside its
+ * chunk layer — lattice index x chunk-count stride, over dims ndims-3 .. 1.
+ */
+uint64_t
+oracle_tile_group_offset(const oracle_dim* dims, uint32_t ndims, uint64_t frame_id)
+{
+    if (!dims || ndims < 3)
+        return UINT64_MAX;
+    uint64_t strides[64];
+    if (ndims > 64)
+        return UINT64_MAX;
+    strides[ndims - 1] = 1;
+    for (uint32_t i = ndims - 1; i > 0; --i) {
+        const uint64_t a = dims[i].array_size_px, c = dims[i].chunk_size_px;
+        if (!c)
+            return UINT64_MAX;
+        strides[i - 1] = strides[i] * ((a + c - 1) / c);
+    }
+    uint64_t offset = 0;
+    for (uint32_t i = ndims - 3; i > 0; --i)
+        offset += (uint64_t)oracle_chunk_lattice_index(dims, ndims, frame_id, i) *
+                  strides[i];
+    return offset;
+}
+
+/*
+ * ArrayDimensions::chunk_internal_offset (array.dimensions.cpp:284-314): the
+ * byte offset of the frame's tile inside its chunk — its index within the
+ * chunk along every non-spatial dim, in chunk strides, times one tile's
+ * bytes (bytes_per_px x Y chunk x X chunk).
+ */
+uint64_t
+oracle_chunk_internal_offset(const oracle_dim* dims,
+                             uint32_t ndims,
+                             uint32_t bytes_per_px,
+                             uint64_t frame_id)
+{
+    if (!dims || ndims < 3 || ndims > 64)
+        return UINT64_MAX;
+    const uint64_t tile_size = (uint64_t)bytes_per_px *
+                               dims[ndims - 1].chunk_size_px *
+                               dims[ndims - 2].chunk_size_px;
+    uint64_t array_strides[64], chunk_strides[64];
+    for (uint32_t i = 0; i < ndims - 2; ++i)
+        array_strides[i] = chunk_strides[i] = 1;
+    uint64_t offset = 0;
+    for (int i = (int)ndims - 3; i > 0; --i) {
+        const uint64_t a = dims[i].array_size_px, c = dims[i].chunk_size_px;
+        if (!a || !c)
+            return UINT64_MAX;
+        const uint64_t internal_idx = (frame_id / array_strides[i]) % a % c;
+        array_strides[i - 1] = array_strides[i] * a;
+        chunk_strides[i - 1] = chunk_strides[i] * c;
+        offset += internal_idx * chunk_strides[i];
+    }
+    if (!dims[0].chunk_size_px)
+        return UINT64_MAX;
+    offset += (frame_id / array_strides[0]) % dims[0].chunk_size_px * chunk_strides[0];
+    return offset * tile_size;
+}

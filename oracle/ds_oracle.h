@@ -112,6 +112,24 @@ int oracle_transpose_frame(int dtype,
                            uint32_t src_cols,
                            void* dst);
 
+/*
+ * Chunk addressing restated from ArrayDimensions (array.dimensions.cpp:
+ * 232-314) over storage-order dims (ndims >= 3, the last two Y and X):
+ * chunk_lattice_index (UINT32_MAX on a bad dim index), tile_group_offset (in
+ * chunks) and chunk_internal_offset (in bytes).
+ */
+uint32_t oracle_chunk_lattice_index(const oracle_dim* dims,
+                                    uint32_t ndims,
+                                    uint64_t frame_id,
+                                    uint32_t dim_index);
+uint64_t oracle_tile_group_offset(const oracle_dim* dims,
+                                  uint32_t ndims,
+                                  uint64_t frame_id);
+uint64_t oracle_chunk_internal_offset(const oracle_dim* dims,
+                                      uint32_t ndims,
+                                      uint32_t bytes_per_px,
+                                      uint64_t frame_id);
+
 /* Stateful downsampler: Downsampler::add_frame / take_frame
  * (downsampler.cpp:306-414) over per-level (width, height, planes). */
 typedef struct oracle_ds oracle_ds;

@@ -72,6 +72,13 @@ def lib():
         L.oracle_shard_index_table.argtypes = [vp, vp, sz, vp]
         L.oracle_ds_level_count.argtypes = [vp, u32]
         L.oracle_ds_level_count.restype = u32
+        u64 = ctypes.c_uint64
+        L.oracle_chunk_lattice_index.argtypes = [ctypes.POINTER(Dim), u32, u64, u32]
+        L.oracle_chunk_lattice_index.restype = u32
+        L.oracle_tile_group_offset.argtypes = [ctypes.POINTER(Dim), u32, u64]
+        L.oracle_tile_group_offset.restype = u64
+        L.oracle_chunk_internal_offset.argtypes = [ctypes.POINTER(Dim), u32, u32, u64]
+        L.oracle_chunk_internal_offset.restype = u64
         _lib = L
     return _lib
 
@@ -258,3 +265,52 @@ def cascade_2d(frame: np.ndarray, n_levels: int, method: int):
         cur = scale_image(cur, method)
         out.append(cur)
     return out
+
+
+def _dim_array(dims):
+    return (Dim * len(dims))(*[Dim(d[0], d[1], d[2], d[3], d[4] if len(d) > 4 else 1.0)
+                               for d in dims])
+
+
+def chunk_lattice_index(dims, frame_id: int, dim_index: int) -> int:
+    """ArrayDimensions::chunk_lattice_index (array.dimensions.cpp:232-262)."""
+    r = lib().oracle_chunk_lattice_index(_dim_array(dims), len(dims), frame_id, dim_index)
+    if r == 0xFFFFFFFF:
+        raise ValueError("invalid dimension index")
+    return int(r)
+
+
+def tile_group_offset(dims, frame_id: int) -> int:
+    """ArrayDimensions::tile_group_offset (array.dimensions.cpp:264-282), in chunks."""
+    return int(lib().oracle_tile_group_offset(_dim_array(dims), len(dims), frame_id))
+
+
+def chunk_internal_offset(dims, bytes_per_px: int, frame_id: int) -> int:
+    """ArrayDimensions::chunk_internal_offset (array.dimensions.cpp:284-314), in bytes."""
+    return int(lib().oracle_chunk_internal_offset(_dim_array(dims), len(dims), bytes_per_px,
+                                                  frame_id))
+
+
+def chunk_frame_offsets(dims, bytes_per_px: int, first_frame: int, n_frames: int):
+    """Where each frame's tile 0 lands in a buffer of whole chunk layers,
+    relative to first_frame's layer: (offsets, chunk_bytes, layer_bytes).
+
+    Array::write_frame_to_chunks_ (array.cpp:563-617) writes tile t of frame
+    k into chunks_[t + tile_group_offset(k)] at chunk_internal_offset(k); one
+    layer holds number_of_chunks_in_memory_ chunks of bytes_per_chunk_
+    (array.dimensions.cpp:168-178); chunk_lattice_index(k, 0) is the layer.
+    """
+    chunk_bytes = bytes_per_px
+    for d in dims:
+        chunk_bytes *= d[2]
+    layer_chunks = 1
+    for d in dims[1:]:
+        layer_chunks *= -(-d[1] // d[2])
+    layer_bytes = layer_chunks * chunk_bytes
+    base = chunk_lattice_index(dims, first_frame, 0)
+    offs = []
+    for k in range(first_frame, first_frame + n_frames):
+        layer = chunk_lattice_index(dims, k, 0) - base
+        offs.append(layer * layer_bytes + tile_group_offset(dims, k) * chunk_bytes +
+                    chunk_internal_offset(dims, bytes_per_px, k))
+    return offs, chunk_bytes, layer_bytes

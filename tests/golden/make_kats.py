@@ -10,10 +10,24 @@ Sources:
   R1 tests/unit-tests/downsampler.cpp
   R2 tests/unit-tests/downsampler-odd-z.cpp
   R3 examples/stream-raw-multiscale-to-filesystem.c (BASELINE config 0)
+  R4 tests/unit-tests/array-dimensions-chunk-internal-offset.cpp
+  R5 tests/unit-tests/array-dimensions-tile-group-offset.cpp
+  R6 tests/unit-tests/array-dimensions-chunk-lattice-index.cpp
+  R7 tests/integration/stream-3d-multiscale-to-filesystem.cpp
+  R8 tests/integration/stream-multiscale-trivial-3rd-dim.cpp
+  R9 tests/integration/stream-2d-multiscale-to-filesystem.cpp
 
-The reference cannot be compiled in this image (src/streaming/downsampler.hh
-includes nlohmann/json.hpp, which is absent) and its Python package cannot be
-built, so no fixture was produced by running reference code.
+R4-R6 (the 203 chunk-addressing assertions) are read straight out of the
+reference test files when this script runs, one fixture entry per EXPECT_EQ
+line with its line number, so the fixture is a transcription, not a
+computation.  R7-R9 evaluate the level expectations with the tests' own
+formulas (cited per line).  The script needs /root/reference only when it is
+re-run here; the tests read the committed JSON alone.
+
+No fixture was produced by running reference code: the downsampler's header
+includes nlohmann/json.hpp, which this image lacks, and a build against a
+stand-in header is not used as an oracle.  The Python package
+cannot be built either (its pybind11 dependencies are absent).
 
 Run: python tests/golden/make_kats.py
 """
@@ -21,6 +35,12 @@ from __future__ import annotations
 
 import json
 import os
+import re
+
+REF = "/root/reference"
+DTYPE_CODES = {"uint8": 0, "uint16": 1, "uint32": 2, "uint64": 3, "int8": 4,
+               "int16": 5, "int32": 6, "int64": 7, "float32": 8, "float64": 9}
+DIM_TYPES = {"Space": 0, "Channel": 1, "Time": 2, "Other": 3}
 
 SPACE, CHANNEL, TIME, OTHER = 0, 1, 2, 3
 DECIMATE, MEAN, MIN, MAX = 0, 1, 2, 3
@@ -189,10 +209,110 @@ def stream_cases():
     return cases
 
 
+def addressing_cases():
+    """R4-R6: every EXPECT_EQ of the three ArrayDimensions addressing tests,
+    with the dimensions and dtype the test builds (array.dimensions.cpp:
+    232-314 is the code under test)."""
+    dim_re = re.compile(r'emplace_back\(\s*"(\w+)",\s*ZarrDimensionType_(\w+),\s*(\d+),'
+                        r'\s*(\d+),\s*(\d+)\)')
+    dt_re = re.compile(r"ArrayDimensions dimensions\(std::move\(dims\), ZarrDataType_(\w+)\)")
+    kat_re = re.compile(r"EXPECT_EQ\(int, dimensions\.(\w+)\(([\d, ]+)\), (\d+)\);")
+    cases = []
+    for tag, fname in (("R4", "array-dimensions-chunk-internal-offset.cpp"),
+                       ("R5", "array-dimensions-tile-group-offset.cpp"),
+                       ("R6", "array-dimensions-chunk-lattice-index.cpp")):
+        path = os.path.join(REF, "tests", "unit-tests", fname)
+        with open(path) as f:
+            text = f.read()
+        dims = [[DIM_TYPES[t], int(a), int(c), int(sh)]
+                for _, t, a, c, sh in dim_re.findall(re.sub(r"\s+", " ", text))]
+        dtype = DTYPE_CODES[dt_re.search(text).group(1)]
+        asserts = []
+        fn = None
+        for no, line in enumerate(text.splitlines(), 1):
+            m = kat_re.search(line)
+            if m:
+                fn = m.group(1)
+                args = [int(x) for x in m.group(2).split(",")]
+                asserts.append({"line": no, "args": args, "expect": int(m.group(3))})
+        cases.append({"name": fname[:-4], "src": f"{tag}:{asserts[0]['line']}-"
+                      f"{asserts[-1]['line']}", "function": fn, "dims": dims,
+                      "dtype": dtype, "asserts": asserts})
+    return cases
+
+
+def integration_cases():
+    """R7-R9: per-level geometry and OME scale the multiscale integration
+    tests expect, evaluated with the tests' own formulas.  `frames` is the
+    frame count each level receives; `scale_rule` says how the test compares
+    scales (R7 compares through `EXPECT_EQ(int, ...)`, i.e. truncated)."""
+    cases = []
+    # R7: t10/5/2 c8/4/2 z6/2/1 (scale 1.4) y48/16/1 (0.9) x64/16/2 (0.9),
+    # u16, Mean, 480 frames (:16-23, :57-125, :49-50)
+    W, H, Z, C, T = 64, 48, 6, 8, 10
+    cw, ch, cz, cc, ct = 16, 16, 2, 4, 5
+    sw, sh, sz, sc, st = 2, 1, 1, 2, 2
+    levels = []
+    w, h, z, prev, acq = W, H, Z, Z, Z * C * T
+    for lv in range(3):
+        if lv:
+            # :244-252: sizes (s+1)/2, acquired frames scaled by planes
+            w, h = (w + 1) // 2, (h + 1) // 2
+            prev, z = z, (z + 1) // 2
+            acq = acq * z // prev
+        t = -(-acq // (C * z))                                   # :254-255
+        nz, ny, nx = -(-z // cz), -(-h // ch), -(-w // cw)         # :257-263
+        levels.append({"sizes": [t, C, z, h, w],                    # :265-271
+                       "chunks": [ct, cc, cz, ch, cw],              # chunk sizes kept
+                       "shards": [st, sc, min(nz, sz), min(ny, sh), min(nx, sw)],  # :265-278
+                       "scales": [1.0, 1.0, 2 ** lv * 1.4, 2 ** lv * 0.9, 2 ** lv * 0.9],
+                       "frames": acq})                              # :229-233
+    cases.append({"name": "stream_3d_multiscale", "src": "R7:16-23,57-125,227-278",
+                  "dtype": U16, "method": MEAN, "scale_rule": "int",
+                  "dims": [[TIME, T, ct, st, 1.0], [CHANNEL, C, cc, sc, 1.0],
+                           [SPACE, Z, cz, sz, 1.4], [SPACE, H, ch, sh, 0.9],
+                           [SPACE, W, cw, sw, 0.9]],
+                  "n_levels": 3, "levels": levels})
+    # R8: t5/5/1 c3/3/1 z1/1/1 (1.36) y48/16/2 (0.85) x64/16/2 (0.85), u16,
+    # Mean, 15 zero frames (:16-41, :44-118); 3 datasets (:141); z scale
+    # stays 1.36 (:177), y/x ~ 0.85 * (size / level size) within 0.01
+    # (:182-206); level shapes are not stated by the test, only through the
+    # scale relation.
+    cases.append({"name": "stream_multiscale_trivial_3rd_dim",
+                  "src": "R8:16-41,44-118,141,160-206", "dtype": U16, "method": MEAN,
+                  "dims": [[TIME, 5, 5, 1, 1.0], [CHANNEL, 3, 3, 1, 1.0],
+                           [SPACE, 1, 1, 1, 1.36], [SPACE, 48, 16, 2, 0.85],
+                           [SPACE, 64, 16, 2, 0.85]],
+                  "n_levels": 3, "frames_in": 15, "zero_frames": True,
+                  "scale_rule": "relative_0.01",
+                  "scale_relation": {"base_scale": [1.0, 1.0, 1.36, 0.85, 0.85],
+                                     "fixed": [0, 1, 2], "ratio": [3, 4]}})
+    # R9: t10/5/2 c8/4/2 y48/16/1 (0.9) x64/16/2 (0.9), u16, Mean, 80 frames
+    # (:16-47, :50-115); per level: sizes ceil(s/2^L) (:216-221), shards
+    # min(n_chunks, shard) (:223-232), scale 2^L*0.9 (:203-208)
+    W, H, C, T = 64, 48, 8, 10
+    levels = []
+    for lv in range(3):
+        w = -(-W // 2 ** lv)
+        h = -(-H // 2 ** lv)
+        levels.append({"sizes": [-(-80 // C), C, h, w],
+                       "chunks": [5, 4, 16, 16],
+                       "shards": [2, 2, min(-(-h // 16), 1), min(-(-w // 16), 2)],
+                       "scales": [1.0, 1.0, 2 ** lv * 0.9, 2 ** lv * 0.9],
+                       "frames": 80})
+    cases.append({"name": "stream_2d_multiscale", "src": "R9:16-47,50-115,184-246",
+                  "dtype": U16, "method": MEAN, "scale_rule": "exact",
+                  "dims": [[TIME, T, 5, 2, 1.0], [CHANNEL, C, 4, 2, 1.0],
+                           [SPACE, H, 16, 1, 0.9], [SPACE, W, 16, 2, 0.9]],
+                  "n_levels": 3, "levels": levels})
+    return cases
+
+
 def main():
     out = {"reference": "acquire-project/acquire-zarr v0.8.1",
            "generator": "tests/golden/make_kats.py",
-           "planner": planner_cases(), "stream": stream_cases()}
+           "planner": planner_cases(), "stream": stream_cases(),
+           "addressing": addressing_cases(), "integration": integration_cases()}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kats.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

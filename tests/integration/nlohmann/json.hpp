@@ -7,6 +7,7 @@
 // never an oracle, never linked into the product and never run.
 #pragma once
 
+#include <cmath> // the real header brings <cmath> in; array.cpp relies on it
 #include <cstddef>
 #include <initializer_list>
 #include <string>
@@ -42,6 +43,8 @@ class json
     void push_back(std::initializer_list<json>) {}
 
     static json object() { return {}; }
+    static json object(std::initializer_list<json>) { return {}; }
     static json array() { return {}; }
+    static json array(std::initializer_list<json>) { return {}; }
 };
 } // namespace nlohmann

@@ -7,10 +7,17 @@ Every lattice buffer is poisoned first: bytes no frame owns must keep the
 poison, every byte a frame owns must equal the oracle's.  The full chunks of
 a completed layer are then compressed where they lie and checked against
 c-blosc itself.
+
+Expected placement never comes from the product: the KAT-dims case takes it
+from the reference's own assertions (tests/golden/reference_kats.json,
+`addressing`), every other case from the oracle's restatement of
+array.dimensions.cpp:232-314 (`oracle.chunk_frame_offsets`), which the CPU
+suite pins to those same assertions (tests/test_reference_addressing.py).
 """
 import numpy as np
 import pytest
 
+import kat_runner
 from gpu_util import empty_device, random_frames, to_device, torch_cuda
 
 pytestmark = pytest.mark.gpu
@@ -25,13 +32,16 @@ def level_dims(dims, geo, L):
     return dims[:-2] + [(SPACE, h, dims[-2][2], 1), (SPACE, w, dims[-1][2], 1)]
 
 
-def expected_lattices(oracle, aqz, dims, geo, frames, dtype, method, first, cap):
+def expected_lattices(oracle, dims, geo, frames, dtype, method, first, cap, placement=None):
     ref = oracle.OracleDownsampler(geo, dtype, method)
     bpp = np.dtype(dtype).itemsize
     outs = [None] + [np.full(cap[L], POISON, np.uint8) for L in range(1, len(geo))]
     offs = [None]
     for L in range(1, len(geo)):
-        o, cb, _ = aqz.chunk_frame_offsets(level_dims(dims, geo, L), bpp, first, len(frames))
+        if placement is not None:
+            offs.append(placement[L])
+            continue
+        o, cb, _ = oracle.chunk_frame_offsets(level_dims(dims, geo, L), bpp, first, len(frames))
         offs.append((o, cb))
     for k, fr in enumerate(frames):
         ref.add_frame(fr)
@@ -47,9 +57,11 @@ def expected_lattices(oracle, aqz, dims, geo, frames, dtype, method, first, cap)
     return outs, offs
 
 
-def run_case(aqz, oracle, dims, dtype, method, first, n, seed):
+def run_case(aqz, oracle, dims, dtype, method, first, n, seed, max_levels=0, placement=None):
+    """`placement[L]` = (offsets, chunk_bytes, layer_bytes) overrides the
+    oracle's addressing for level L."""
     torch = torch_cuda()
-    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    geo = aqz.level_geometry(aqz.plan_levels(dims, max_levels))
     assert len(geo) >= 2
     H, W = dims[-2][1], dims[-1][1]
     rng = np.random.default_rng(seed)
@@ -57,11 +69,15 @@ def run_case(aqz, oracle, dims, dtype, method, first, n, seed):
     bpp = np.dtype(dtype).itemsize
     cap = [0]
     for L in range(1, len(geo)):
-        o, cb, lb = aqz.chunk_frame_offsets(level_dims(dims, geo, L), bpp, first, n)
+        if placement is not None:
+            o, cb, lb = placement[L]
+        else:
+            o, cb, lb = oracle.chunk_frame_offsets(level_dims(dims, geo, L), bpp, first, n)
         # the layers this batch touches
         cap.append((max(o) // lb + 1) * lb)
-    want, offs = expected_lattices(oracle, aqz, dims, geo, list(frames), dtype, method, first,
-                                   cap)
+    want, offs = expected_lattices(oracle, dims, geo, list(frames), dtype, method, first,
+                                   cap, None if placement is None else
+                                   [None] + [placement[L][:2] for L in range(1, len(geo))])
     ds = aqz.Downsampler(geo, dtype, method, device=0)
     d_in = to_device(frames)
     bufs = [None] + [empty_device(cap[L]) for L in range(1, len(geo))]
@@ -105,6 +121,43 @@ def test_channel_chunks(aqz, oracle, method):
     chunk and its place in it both depend on the channel."""
     dims = [(TIME, 0, 2, 1), (CHANNEL, 3, 2, 1), (SPACE, 256, 64, 1), (SPACE, 300, 64, 1)]
     run_case(aqz, oracle, dims, np.uint16, aqz.METHODS[method], 1, 9, seed=7)
+
+
+def kat_placement():
+    """Frame k's tile-0 offset in a lattice of the KAT dims (t 0/5, c 3/2,
+    z 5/2, y 48/16, x 64/16, u16), built only from the reference's asserted
+    values: chunk_lattice_index(k, 0) layers, tile_group_offset(k) chunks and
+    chunk_internal_offset(k) bytes (array-dimensions-*.cpp)."""
+    kats = {c["function"]: c for c in kat_runner.load()["addressing"]}
+    cio = {a["args"][0]: a["expect"] for a in kats["chunk_internal_offset"]["asserts"]}
+    tgo = {a["args"][0]: a["expect"] for a in kats["tile_group_offset"]["asserts"]}
+    layer = {a["args"][0]: a["expect"] for a in kats["chunk_lattice_index"]["asserts"]
+             if a["args"][1] == 0}
+    assert kats["chunk_internal_offset"]["dtype"] == 1  # offsets in u16 bytes
+    chunk_bytes = 2 * 5 * 2 * 2 * 16 * 16      # bytes_per_chunk_, array.dimensions.cpp:171
+    layer_bytes = 2 * 3 * 3 * 4 * chunk_bytes  # number_of_chunks_in_memory_, :175
+    frames = sorted(cio)
+    assert frames == list(range(76)) and sorted(tgo) == frames
+    # the lattice-index KAT names the layer of 17 of these frames; the rest
+    # share layer 0 (frames 0..74 are t 0..4, one T chunk)
+    offs = [layer.get(k, 0 if k < 75 else None) * layer_bytes + tgo[k] * chunk_bytes + cio[k]
+            for k in frames]
+    return offs, chunk_bytes, layer_bytes
+
+
+def test_kat_dims_placement(aqz, oracle):
+    """The reference's addressing test dims as a pyramid level: a 96x128 base
+    (y/x chunks 16) gives level 1 = t 0/5, c 3/2, z 5/2, y 48/16, x 64/16 —
+    the dims of tests/unit-tests/array-dimensions-*.cpp (z is typed Channel so
+    the planner keeps its 5 planes; the addressing reads sizes and chunks
+    only).  All 76 frames those tests name go in one batch, frame 75 into the
+    second layer; every tile must land where the asserted values put it."""
+    dims = [(TIME, 0, 5, 1), (CHANNEL, 3, 2, 1), (CHANNEL, 5, 2, 1), (SPACE, 96, 16, 1),
+            (SPACE, 128, 16, 1)]
+    geo = aqz.level_geometry(aqz.plan_levels(dims, 1))
+    assert geo == [(128, 96, 5), (64, 48, 5)]
+    run_case(aqz, oracle, dims, np.uint16, aqz.METHODS["mean"], 0, 76, seed=21, max_levels=1,
+             placement=[None, kat_placement()])
 
 
 def test_deep_pyramid_chains(aqz, oracle):

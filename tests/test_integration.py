@@ -17,11 +17,19 @@ src/streaming sources.  Then:
 * cmake/hip.cmake configures a toy target for AQZ_DOWNSAMPLER=hip/cpu and
   rejects anything else.
 
-nlohmann/json is not in this image, so tests/integration/nlohmann/json.hpp is
-a compile-only stand-in: nothing built here computes anything or runs.  The
-reference's array.cpp needs crc32c and zstd headers, also absent, so its two
-patched hooks are checked as text only.  Skipped when /root/reference is
-absent (the GPU box)."""
+* the patched array.cpp (its three tiled-frame hooks) compiles in both modes;
+* the tiled chunk writer (array.tiled.cpp) RUNS on the reference's own
+  ArrayDimensions and Chunk (array.dimensions.cpp, chunk.cpp, zarr.common.cpp,
+  compiled from /root/reference): chunk bytes, has_data and the bytes written
+  per frame must equal what write_frame_to_chunks_ (array.cpp:507-622) leaves
+  — the oracle's tiling placed by the oracle's KAT-pinned addressing — on
+  ragged frames, several layers and N-D chunk lattices.
+
+nlohmann/json and google/crc32c are not in this image, so
+tests/integration/nlohmann/json.hpp and tests/integration/crc32c/crc32c.h are
+compile-only stand-ins: nothing built with them is linked or run.  blosc.h and
+zstd.h are the image's own (/opt/conda/include).  Skipped when /root/reference
+is absent (the GPU box)."""
 import os
 import shutil
 import subprocess
@@ -32,6 +40,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 STUB = os.path.join(ROOT, "tests", "integration")
 LIB_DIR = os.path.join(ROOT, "acquire-zarr_amd")
+CONDA_INC = "/opt/conda/include"   # blosc.h, zstd.h (part of the image)
+CONDA_LIB = "/opt/conda/lib"
 
 pytestmark = pytest.mark.skipif(
     not os.path.exists(os.path.join(REF, "src", "streaming", "downsampler.hh")),
@@ -57,7 +67,7 @@ def gxx(tree, args, defines=("AQZ_DOWNSAMPLER_HIP",)):
     cmd += [f"-D{d}" for d in defines]
     cmd += ["-I", STUB, "-I", os.path.join(ROOT, "include"),
             "-I", str(tree / "include"), "-I", str(tree / "src" / "streaming"),
-            "-I", str(tree / "src" / "logger")] + list(args)
+            "-I", str(tree / "src" / "logger"), "-idirafter", CONDA_INC] + list(args)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, " ".join(cmd) + "\n" + r.stderr[-4000:]
     return r
@@ -72,6 +82,9 @@ def test_patch_applies_and_keeps_reference_bodies_out(tree):
     a = (tree / "src" / "streaming" / "array.cpp").read_text()
     assert "return write_tiles_to_chunks_(frame);" in a
     assert "tiled_ ? bytes_of_frame(*config_->dimensions, config_->dtype)" in a
+    # the Ok/PartialWrite result compares with the payload, not the tiled
+    # buffer's size (which includes the zero overhang)
+    assert "return bytes_written == nbytes_data ? WriteResult::Ok" in a
     top = (tree / "CMakeLists.txt").read_text()
     assert "include(cmake/hip.cmake)" in top
     streaming = (tree / "src" / "streaming" / "CMakeLists.txt").read_text()
@@ -147,8 +160,110 @@ def test_callers_compile(tree):
 
 def test_cpu_build_unchanged(tree):
     # AQZ_DOWNSAMPLER=cpu: the patched files compile to the reference's code
-    for f in ("downsampler.cpp", "multiscale.array.cpp"):
-        gxx(tree, ["-fsyntax-only", str(tree / "src" / "streaming" / f)], defines=())
+    for f in ("downsampler.cpp", "multiscale.array.cpp", "array.cpp"):
+        gxx(tree, ["-fopenmp", "-fsyntax-only", str(tree / "src" / "streaming" / f)],
+            defines=())
+
+
+def test_patched_array_cpp_compiles(tree):
+    # the three hooks (payload size, Ok/PartialWrite, tiled dispatch) in the
+    # HIP build of the reference's own array.cpp
+    gxx(tree, ["-fopenmp", "-fsyntax-only", str(tree / "src" / "streaming" / "array.cpp")])
+
+
+@pytest.fixture(scope="module")
+def harness(tree, tmp_path_factory):
+    """tests/integration/tiled_writer_harness.cpp linked with the reference's
+    array.dimensions.cpp, chunk.cpp, zarr.common.cpp and logger.cpp and the
+    drop-in's array.tiled.cpp (placement only)."""
+    out = tmp_path_factory.mktemp("harness")
+    # libblosc's RPATH is $ORIGIN: a private copy with its codecs keeps
+    # /opt/conda/lib (and its older libstdc++) off the harness's search path
+    libs = out / "lib"
+    libs.mkdir()
+    for name in ("libblosc.so.1", "liblz4.so.1", "libz.so.1", "libzstd.so.1"):
+        shutil.copy(os.path.join(CONDA_LIB, name), libs / name)
+    os.symlink("libblosc.so.1", libs / "libblosc.so")
+    os.symlink("libzstd.so.1", libs / "libzstd.so")
+    srcs = [tree / "src" / "streaming" / "array.dimensions.cpp",
+            tree / "src" / "streaming" / "chunk.cpp",
+            tree / "src" / "streaming" / "zarr.common.cpp",
+            tree / "src" / "logger" / "logger.cpp",
+            tree / "src" / "streaming" / "array.tiled.cpp",
+            os.path.join(STUB, "tiled_writer_harness.cpp")]
+    exe = out / "tiled_writer_harness"
+    gxx(tree, ["-O1", "-fopenmp", "-DAQZ_TILED_STANDALONE", "-o", str(exe)] +
+        [str(x) for x in srcs] + ["-L", str(libs), "-lblosc", "-lzstd", f"-Wl,-rpath,{libs}",
+                                  "-lpthread"], defines=())
+    return exe
+
+
+SPACE, CHANNEL, TIME = 0, 1, 2
+
+
+def _run_harness(exe, tmp_path, oracle, dims, dtype, n_frames, seed):
+    import numpy as np
+    np_dt = np.dtype(dtype)
+    bpp = np_dt.itemsize
+    H, W = dims[-2][1], dims[-1][1]
+    tr, tc = dims[-2][2], dims[-1][2]
+    rng = np.random.default_rng(seed)
+    frames = rng.integers(1, 200, (n_frames, H, W)).astype(dtype)
+    frames[1::3, :tr, :] = 0            # whole zero tile rows in some frames
+    if n_frames > 4:
+        frames[4] = 0                   # and one all-zero frame
+    tiles = [oracle.tile_frame(f, tr, tc)[0] for f in frames]
+    blob = b"".join(t.tobytes() for t in tiles)
+    (tmp_path / "tiles.bin").write_bytes(blob)
+    spec = f"{len(dims)} {bpp} {oracle.dtype_code(dtype)} {n_frames}\n" + \
+        "".join(f"{t} {a} {c} {s}\n" for t, a, c, s in dims)
+    r = subprocess.run([str(exe), str(tmp_path / "tiles.bin"), str(tmp_path / "chunks.bin")],
+                       input=spec, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    written = [int(ln.split()[2]) for ln in r.stdout.splitlines() if ln.startswith("frame ")]
+    # what the patched write_frame compares with: one frame's payload, so a
+    # ragged level returns WriteResult::Ok, never PartialWrite
+    assert written == [H * W * bpp] * n_frames
+    # expected chunk layers: the oracle's tiles at the oracle's offsets
+    # (array.dimensions.cpp:232-314, pinned to the reference's KATs)
+    offs, cb, lb = oracle.chunk_frame_offsets(dims, bpp, 0, n_frames)
+    n_layers = max(offs) // lb + 1
+    want = np.zeros(n_layers * lb, np.uint8)
+    touched = np.zeros(n_layers * (lb // cb), bool)
+    tb = tr * tc * bpp
+    for k in range(n_frames):
+        for t in range(tiles[k].shape[0]):
+            at = offs[k] + t * cb
+            want[at:at + tb] = tiles[k][t].view(np.uint8).reshape(-1)
+            touched[at // cb] = True
+    got = np.frombuffer((tmp_path / "chunks.bin").read_bytes(), np.uint8)
+    assert got.size == n_layers * (lb // cb) * (cb + 1)
+    got = got.reshape(-1, cb + 1)
+    state, data = got[:, 0], got[:, 1:].reshape(-1)
+    np.testing.assert_array_equal(data, want)
+    want_state = np.where(~touched, 0,
+                          np.where(want.reshape(-1, cb).any(axis=1), 2, 1))
+    np.testing.assert_array_equal(state, want_state)
+    return written
+
+
+@pytest.mark.parametrize("dims,dtype,n", [
+    # T/Y/X, ragged level (the 3000x3000 shape class: not a multiple of the
+    # chunk), 3 frames per chunk, 3 layers with a partial last one
+    ([(TIME, 0, 3, 1), (SPACE, 75, 32, 1), (SPACE, 93, 32, 1)], "uint16", 8),
+    # the reference's addressing-test dims (t 0/5, c 3/2, z 5/2, y 48/16,
+    # x 64/16): all 76 frames its KATs name, the 76th opens layer 2
+    ([(TIME, 0, 5, 1), (CHANNEL, 3, 2, 1), (CHANNEL, 5, 2, 1), (SPACE, 48, 16, 1),
+      (SPACE, 64, 16, 1)], "uint16", 76),
+    # T/C/Y/X with ragged XY and channels chunked 2 of 3, f32
+    ([(TIME, 0, 2, 1), (CHANNEL, 3, 2, 1), (SPACE, 40, 16, 1), (SPACE, 37, 16, 1)],
+     "float32", 9),
+    # single-tile frames narrower than a chunk, u8
+    ([(TIME, 0, 4, 1), (SPACE, 7, 8, 1), (SPACE, 5, 8, 1)], "uint8", 6),
+])
+def test_tiled_writer_runs_on_reference_chunks(harness, tmp_path, oracle, dims, dtype, n):
+    import numpy as np
+    _run_harness(harness, tmp_path, oracle, dims, np.dtype(dtype), n, seed=len(dims) + n)
 
 
 def _configure(tree, tmp_path, value):
