@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <array>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -156,7 +157,15 @@ struct aqz_ds
     std::vector<std::pair<uint32_t, uint32_t>> tiling;
     std::vector<std::pair<void*, void*>> tslot;
     std::vector<std::pair<uint8_t*, uint8_t*>> tflags; // pinned, kernel-written
+    // per level and tiled slot: flag bytes each half can hold, and the flag
+    // bytes per tile of the frame tiled there (tile_slices for the tile
+    // kernel, cascade_tiled_slots for the one-pass tiled cascade)
+    std::vector<std::array<size_t, 2>> tflag_cap;
+    std::vector<std::array<uint32_t, 2>> tflag_slices;
     std::vector<int> tiled_for;
+    // $AQZ_STREAM_TILE_PASS=1: eager tiling as a tile pass behind the
+    // row-major cascade (the round-2 path), for A/B
+    bool tile_pass = false;
     // eager tiled readback (aqz_ds::eager): pinned copy of a level's tiles,
     // queued right behind its tile kernel, and which slot's frame it holds
     std::vector<uint8_t*> h_tiles;
@@ -264,11 +273,12 @@ tile_geom(const aqz_ds* ds, uint32_t L, uint32_t tr, uint32_t tc)
     return { nt, nt * tr * tc * ds->bpp, nt * aqz::tile_slices(tr, tc) };
 }
 
-// One flag per tile: the OR of its slice flags (pinned, kernel-written).
+// One flag per tile: the OR of its `slices` flag bytes (pinned,
+// kernel-written, tile-major).
 void
-reduce_slice_flags(const TileGeom& g, const uint8_t* flags, uint8_t* tile_nonzero)
+reduce_slice_flags(const TileGeom& g, size_t slices, const uint8_t* flags,
+                   uint8_t* tile_nonzero)
 {
-    const size_t slices = g.flag_bytes / g.n_tiles;
     for (size_t t = 0; t < g.n_tiles; ++t) {
         uint8_t any = 0;
         for (size_t q = 0; q < slices; ++q)
@@ -280,15 +290,15 @@ reduce_slice_flags(const TileGeom& g, const uint8_t* flags, uint8_t* tile_nonzer
 // D2H of tiles already laid out on the device, then one flag per tile from
 // its slice flags (pinned, written by the tile kernel).
 int
-tiles_to_host(aqz_ds* ds, const TileGeom& g, const void* d_tiles, const uint8_t* flags,
-              void* dst, uint8_t* tile_nonzero)
+tiles_to_host(aqz_ds* ds, const TileGeom& g, size_t slices, const void* d_tiles,
+              const uint8_t* flags, void* dst, uint8_t* tile_nonzero)
 {
     HIP_TRY(ds,
             hipMemcpyAsync(dst, d_tiles, g.tile_bytes, hipMemcpyDeviceToHost, ds->stream),
             "hipMemcpyAsync D2H");
     HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
     if (tile_nonzero)
-        reduce_slice_flags(g, flags, tile_nonzero);
+        reduce_slice_flags(g, slices, flags, tile_nonzero);
     return AQZ_OK;
 }
 
@@ -316,7 +326,8 @@ tile_to_host(aqz_ds* ds, const void* d_frame, const aqz_level_desc& lv, uint32_t
             aqz::launch_tile_frame_sliced(ds->dtype, d_frame, lv.width, lv.height, tile_rows,
                                           tile_cols, ds->d_tiles, ds->h_flags, ds->stream),
             "tile kernel");
-    return tiles_to_host(ds, g, ds->d_tiles, ds->h_flags, dst, tile_nonzero);
+    return tiles_to_host(ds, g, g.flag_bytes / g.n_tiles, ds->d_tiles, ds->h_flags, dst,
+                         tile_nonzero);
 }
 
 // Working buffer for a level-L result: the caller's batch slot when the
@@ -330,9 +341,11 @@ level_target(aqz_ds* ds, uint32_t L, const Sink& sink)
     return ds->out_slot(L);
 }
 
-// emplace_downsampled_frame_ (downsampler.cpp:599-605).
+// emplace_downsampled_frame_ (downsampler.cpp:599-605).  `pretiled`: the
+// one-pass tiled cascade has already written this frame's tiles and flags
+// into the tiled slot paired with its slot.
 int
-emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink)
+emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink, bool pretiled = false)
 {
     ++ds->count[level];
     void* want = level_target(ds, level, sink);
@@ -352,7 +365,9 @@ emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink)
         const int k = (want == ds->slot[level].first) ? 0 : 1;
         ds->cached[level] = k;
         const auto [tr, tc] = ds->tiling[level];
-        if (tr) {
+        if (tr && pretiled) {
+            ds->tiled_for[level] = k;
+        } else if (tr) {
             // queue the chunk tiling right behind the pyramid (§8(f) row 2)
             void* tb = k == 0 ? ds->tslot[level].first : ds->tslot[level].second;
             uint8_t* fb = k == 0 ? ds->tflags[level].first : ds->tflags[level].second;
@@ -362,8 +377,69 @@ emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink)
                                                   ds->stream),
                     "tile kernel");
             ds->tiled_for[level] = k;
+            ds->tflag_slices[level][k] = aqz::tile_slices(tr, tc);
         }
     }
+    return AQZ_OK;
+}
+
+// One run of k pure-XY levels from L, every one of them tiled: the tiled
+// cascade writes each level row-major into its free slot (the next run's
+// input and take_frame's copy) and chunk-tiled, zero scan included, into the
+// tiled slot paired with it — one launch instead of the cascade plus a tile
+// pass per level.  *launched is false when the geometry needs the separate
+// tile pass (nothing was queued but, at most, a flag clear).
+int
+launch_run_tiled(aqz_ds* ds, uint32_t L, uint32_t k, const void* cur,
+                 const aqz::LevelOut* outs, bool* launched)
+{
+    *launched = false;
+    if (ds->tile_pass)
+        return AQZ_OK;
+    const aqz_level_desc& a = ds->lv[L - 1];
+    if (aqz::cascade_tiled_cols(ds->dtype, a.width) !=
+        aqz::cascade_pick_cols(ds->dtype, cur, elems(ds, L - 1), a.width, a.height, outs, int(k)))
+        return AQZ_OK;
+    aqz::TiledOut t[aqz::kMaxFusedLevels];
+    uint32_t slices[aqz::kMaxFusedLevels];
+    int kk[aqz::kMaxFusedLevels];
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t l = L + j;
+        const auto [tr, tc] = ds->tiling[l];
+        if (!tr)
+            return AQZ_OK;
+        const int s = outs[j].ptr == ds->slot[l].first ? 0 : 1;
+        const uint32_t slots = aqz::cascade_tiled_slots(ds->dtype, a.width, int(k), int(j + 1),
+                                                        tr, tc, nullptr);
+        if (!slots)
+            return AQZ_OK; // one OR-ed flag per tile would need a clear of pinned memory
+        slices[j] = slots;
+        const TileGeom g = tile_geom(ds, l, tr, tc);
+        const size_t need = g.n_tiles * slices[j];
+        uint8_t*& fb = s == 0 ? ds->tflags[l].first : ds->tflags[l].second;
+        if (ds->tflag_cap[l][s] < need) {
+            // the half is free (its slot is not the cached one); earlier
+            // kernels may still write it
+            HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+            (void)hipHostFree(fb);
+            fb = nullptr;
+            ds->tflag_cap[l][s] = 0;
+            HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&fb), need, hipHostMallocDefault),
+                    "hipHostMalloc flags");
+            ds->tflag_cap[l][s] = need;
+        }
+        kk[j] = s;
+        t[j] = { s == 0 ? ds->tslot[l].first : ds->tslot[l].second, tr, tc, fb };
+    }
+    const hipError_t e = aqz::launch_cascade_tiled(ds->dtype, ds->method, cur, elems(ds, L - 1),
+                                                   a.width, a.height, outs, t, int(k), 1,
+                                                   ds->stream);
+    if (e == hipErrorInvalidValue)
+        return AQZ_OK;
+    HIP_TRY(ds, e, "tiled cascade kernel");
+    for (uint32_t j = 0; j < k; ++j)
+        ds->tflag_slices[L + j][kk[j]] = slices[j];
+    *launched = true;
     return AQZ_OK;
 }
 
@@ -404,8 +480,14 @@ process_frame(aqz_ds* ds, const void* d_frame, const Sink& sink)
                 outs[j] = { level_target(ds, L + j, sink), elems(ds, L + j),
                             ds->lv[L + j].width, ds->lv[L + j].height };
             const aqz_level_desc& a = ds->lv[L - 1];
-            if (aqz::cascade_supported(ds->dtype, cur, elems(ds, L - 1), a.width, a.height,
-                                       outs, int(k))) {
+            bool pretiled = false;
+            if (!sink.batch)
+                if (int rc = launch_run_tiled(ds, L, k, cur, outs, &pretiled))
+                    return rc;
+            if (pretiled) {
+                // levels and their tiles written by the tiled cascade
+            } else if (aqz::cascade_supported(ds->dtype, cur, elems(ds, L - 1), a.width,
+                                              a.height, outs, int(k))) {
                 HIP_TRY(ds,
                         aqz::launch_cascade(ds->dtype, ds->method, cur,
                                             elems(ds, L - 1), a.width, a.height,
@@ -425,7 +507,7 @@ process_frame(aqz_ds* ds, const void* d_frame, const Sink& sink)
                 }
             }
             for (uint32_t j = 0; j < k; ++j) {
-                int rc = emit(ds, L + j, outs[j].ptr, sink);
+                int rc = emit(ds, L + j, outs[j].ptr, sink, pretiled);
                 if (rc)
                     return rc;
             }
@@ -939,6 +1021,9 @@ aqz_ds_create(const aqz_level_desc* levels,
         ds->tiling.assign(n_levels, { 0, 0 });
         ds->tslot.assign(n_levels, { nullptr, nullptr });
         ds->tflags.assign(n_levels, { nullptr, nullptr });
+        ds->tflag_cap.assign(n_levels, { 0, 0 });
+        ds->tflag_slices.assign(n_levels, { 1, 1 });
+        ds->tile_pass = env_flag("AQZ_STREAM_TILE_PASS");
         ds->tiled_for.assign(n_levels, -1);
         ds->h_tiles.assign(n_levels, nullptr);
         ds->htile_for.assign(n_levels, -1);
@@ -1166,6 +1251,7 @@ aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t
         (void)hipHostFree(tf.first);
         (void)hipHostFree(tf.second);
         tf = { nullptr, nullptr };
+        ds->tflag_cap[level] = { 0, 0 };
         (void)hipHostFree(ds->h_tiles[level]);
         ds->h_tiles[level] = nullptr;
         ds->htile_for[level] = -1;
@@ -1183,6 +1269,7 @@ aqz_ds_set_level_tiling(aqz_ds* ds, uint32_t level, uint32_t tile_rows, uint32_t
                                   hipHostMallocDefault), "hipHostMalloc flags");
         HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&tf.second), g.flag_bytes,
                                   hipHostMallocDefault), "hipHostMalloc flags");
+        ds->tflag_cap[level] = { g.flag_bytes, g.flag_bytes };
         if (ds->eager)
             HIP_TRY(ds, hipHostMalloc(reinterpret_cast<void**>(&ds->h_tiles[level]),
                                       g.tile_bytes, hipHostMallocDefault),
@@ -1232,12 +1319,13 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
             HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
             std::memcpy(dst, ds->h_tiles[level], g.tile_bytes);
             if (tile_nonzero)
-                reduce_slice_flags(g, k == 0 ? ds->tflags[level].first
-                                             : ds->tflags[level].second, tile_nonzero);
+                reduce_slice_flags(g, ds->tflag_slices[level][k],
+                                   k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
+                                   tile_nonzero);
         } else if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
                    ds->tiled_for[level] == k) {
             // tiled when the frame was emitted (aqz_ds_set_level_tiling)
-            if (int rc = tiles_to_host(ds, g,
+            if (int rc = tiles_to_host(ds, g, ds->tflag_slices[level][k],
                                        k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
                                        k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
                                        dst, tile_nonzero))

@@ -86,37 +86,55 @@ def aggregate_gpix(world: int, frames_per_rank: int, W: int, H: int, steps: int,
 
 def scatter_frames(pool, local, frame_bytes: int, frames_per_rank: int, dist,
                    rank: int, world: int):
-    """Batched-frame config F over xGMI: rank 0 holds every rank's frames
-    contiguously in `pool` (rank r's block at r*frames_per_rank) and sends
-    each block to its rank with point-to-point ops (RCCL send/recv under
-    the nccl backend).  Returns the tensor this rank computes on."""
+    """Batched-frame config F over xGMI: rank 0 holds every
+    rank's frames contiguously in `pool` (rank r's block at r*frames_per_rank)
+    and sends each block to its rank as ONE grouped point-to-point batch
+    (dist.batch_isend_irecv: ncclGroupStart / ncclSend x N / ncclGroupEnd
+    under RCCL, so every peer's xGMI link streams at once).  Returns the
+    tensor this rank computes on."""
     blk = frames_per_rank * frame_bytes
     if rank == 0:
-        reqs = [dist.isend(pool[r * blk:(r + 1) * blk], dst=r) for r in range(1, world)]
-        for q in reqs:
+        ops = [dist.P2POp(dist.isend, pool[r * blk:(r + 1) * blk], r) for r in range(1, world)]
+        mine = pool[:blk]
+    else:
+        ops = [dist.P2POp(dist.irecv, local[:blk], 0)]
+        mine = local[:blk]
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
             q.wait()
-        return pool[:blk]
-    dist.irecv(local[:blk], src=0).wait()
-    return local[:blk]
+    return mine
 
 
 def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
-    """Send every rank's level outputs back to rank 0, which lays rank r's
-    block of level L at pool_levels[L][r*len:(r+1)*len] (rank 0's own block
-    is copied locally)."""
-    reqs = []
+    """Every rank's level outputs back to rank 0 in one grouped p2p batch
+    (all levels, all peers); rank 0 lays rank r's block of level L at
+    pool_levels[L][r*len:(r+1)*len] (its own block is copied locally).
+    Blocks are contiguous frame ranges in rank order, so rank 0's levels come
+    back in acquisition order — the order Array::write_frame requires
+    (array.cpp:179-189 rejects out-of-order frame ids)."""
+    ops = []
     for L, buf in enumerate(level_bufs):
         if buf is None:
             continue
         n = buf.numel()
         if rank == 0:
             pool_levels[L][:n].copy_(buf)
-            reqs += [dist.irecv(pool_levels[L][r * n:(r + 1) * n], src=r)
-                     for r in range(1, world)]
+            ops += [dist.P2POp(dist.irecv, pool_levels[L][r * n:(r + 1) * n], r)
+                    for r in range(1, world)]
         else:
-            reqs.append(dist.isend(buf, dst=0))
-    for q in reqs:
-        q.wait()
+            ops.append(dist.P2POp(dist.isend, buf, 0))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+
+
+def resequence(per_rank_frames, world: int):
+    """Acquisition order from a round-robin deal (rank_frames): frame i came
+    back as the (i // world)-th frame of rank i % world.  The host side of
+    frame sharding without a gather: levels reach the writer
+    in frame-id order, as Array::write_frame requires (array.cpp:179-189)."""
+    total = sum(len(f) for f in per_rank_frames)
+    return [per_rank_frames[i % world][i // world] for i in range(total)]
 
 
 def algorithmic_bytes(geo, counts, frames: int, method: str, bpp: int, tile=None):
@@ -325,13 +343,29 @@ def main():
     else:
         batch = ds.batch_call(d_in.data_ptr(), B, out_ptrs, sptr)
 
-    def step():
+    def step(ev=None):
+        """One step; `ev` = (start, kernel_start, kernel_end, end) events
+        recorded on the launch stream, so that in --xgmi-scatter mode the
+        kernel's own time is separate from the p2p scatter/gather around it
+        (the p2p work is joined onto `stream` by wait())."""
         if xgmi:
+            if ev:
+                ev[0].record(stream)
             mine = scatter_frames(pool, d_in, frame_bytes, B, dist, rank, world)
+            if ev:
+                ev[1].record(stream)
             counts[:] = ds.run_device_batch(mine.data_ptr(), B, out_ptrs, sptr)
+            if ev:
+                ev[2].record(stream)
             gather_levels(outs, pool_levels, dist, rank, world)
+            if ev:
+                ev[3].record(stream)
         else:
+            if ev:
+                ev[1].record(stream)
             counts[:] = batch()
+            if ev:
+                ev[2].record(stream)
 
     if args.pmc_child:
         # launched under `rocprofv3 --pmc` by measure_traffic(): launches only
@@ -381,26 +415,33 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # per-launch kernel timing with HIP events on the launch stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    # per-launch kernel timing with HIP events on the launch stream (in
+    # --xgmi-scatter mode the kernel's own pair sits between the p2p batches)
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
            for _ in range(args.steps)]
 
     def timed_step(i):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
+        step(evs[i])
 
     elapsed = timed_region(timed_step, args.steps, dist, torch.cuda.synchronize)
-    launch_ms = [a.elapsed_time(b) for a, b in evs]
+    launch_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    comm_ms = ([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3]) for e in evs]
+               if xgmi else None)
     dev = "cuda" if (dist is not None and dist.get_backend() == "nccl") else "cpu"
     elapsed = max_over_ranks(elapsed, dist, dev)
-    # every rank's average launch (us), gathered for the N > 1 line
+    # every rank's average launch (us) and p2p time (ms), gathered for the
+    # N > 1 line
     rank_launch_us = [float(np.mean(launch_ms)) * 1e3]
+    rank_comm_ms = [float(np.mean(comm_ms))] if xgmi else None
     if dist is not None:
-        t = torch.zeros(world, dtype=torch.float64, device=dev)
+        t = torch.zeros(2 * world, dtype=torch.float64, device=dev)
         t[rank] = rank_launch_us[0]
+        if xgmi:
+            t[world + rank] = rank_comm_ms[0]
         dist.all_reduce(t)
-        rank_launch_us = [float(x) for x in t.cpu()]
+        rank_launch_us = [float(x) for x in t[:world].cpu()]
+        if xgmi:
+            rank_comm_ms = [float(x) for x in t[world:].cpu()]
 
     ms_per_step = elapsed / args.steps * 1e3
     value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
@@ -420,9 +461,14 @@ def main():
                 "min_launch_us": round(min(launch_ms) * 1e3, 2)}
 
     if world > 1:
+        # kernel-only fractions: in --xgmi-scatter mode the p2p time is
+        # reported beside them (comm_ms_per_step), never blended in
         roofline["per_rank"] = [{"rank": r, "avg_launch_us": round(u, 2),
                                  "frac": round(alg_bytes / (u * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
                                 for r, u in enumerate(rank_launch_us)]
+        if xgmi:
+            for r, c in enumerate(rank_comm_ms):
+                roofline["per_rank"][r]["comm_ms_per_step"] = round(c, 4)
 
     ceiling = measure_ceiling(torch, stream, d_in, read_bytes, alg_bytes - read_bytes,
                               max(5, args.steps // 2))
@@ -506,6 +552,7 @@ def main():
                                          f"world_size={dist.get_world_size()}"
                                          if dist is not None else ""),
                        "check": check},
+            "comm_ms_per_step": (round(max(rank_comm_ms), 4) if xgmi else None),
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
             "e2e": e2e,

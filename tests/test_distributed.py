@@ -134,3 +134,27 @@ def test_xgmi_scatter_gather_logic(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_resequence_round_robin(world):
+    """Frames dealt round-robin come back in acquisition order: what the
+    host must hand Array::write_frame (array.cpp:179-189)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    total = 23
+    per_rank = [[("frame", i) for i in bench.rank_frames(total, r, world)] for r in range(world)]
+    assert bench.resequence(per_rank, world) == [("frame", i) for i in range(total)]
+
+
+def test_scatter_gather_are_grouped():
+    """scatter_frames/gather_levels issue their point-to-point ops as one
+    grouped batch (dist.batch_isend_irecv — RCCL group semantics, SURVEY
+    §8(e)), never one isend/irecv at a time."""
+    import inspect
+    sys.path.insert(0, ROOT)
+    import bench
+    for fn in (bench.scatter_frames, bench.gather_levels):
+        src = inspect.getsource(fn)
+        assert "batch_isend_irecv" in src and "P2POp" in src
+        assert "dist.isend(" not in src and "dist.irecv(" not in src
