@@ -33,7 +33,7 @@ METHODS = {"decimate": DECIMATE, "mean": MEAN, "min": MIN, "max": MAX}
 EXPORTS = (
     "aqz_plan_levels", "aqz_ds_create", "aqz_ds_destroy", "aqz_ds_add_frame",
     "aqz_ds_add_device_frame", "aqz_ds_take_frame", "aqz_ds_run_device_batch",
-    "aqz_ds_last_batch_kind", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
+    "aqz_ds_last_batch_kind", "aqz_ds_stream_tiled_runs", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
     "aqz_ds_run_device_batch_tiled", "aqz_ds_tiled_flag_slots",
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
     "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_set_input_transpose",
@@ -162,6 +162,8 @@ def lib() -> ctypes.CDLL:
                                         ctypes.POINTER(u32)]
     L.aqz_ds_last_batch_kind.argtypes = [vp]
     L.aqz_ds_last_batch_kind.restype = i32
+    L.aqz_ds_stream_tiled_runs.argtypes = [vp]
+    L.aqz_ds_stream_tiled_runs.restype = ctypes.c_uint64
     L.aqz_ds_level_bytes.argtypes = [vp, u32]
     L.aqz_ds_level_bytes.restype = sz
     L.aqz_ds_level_count.argtypes = [vp]
@@ -334,6 +336,10 @@ class Downsampler:
         some runs on batched single-level kernels, 4 fused 2-D cascade writing
         chunk tiles, -1 none."""
         return lib().aqz_ds_last_batch_kind(self._h)
+
+    def stream_tiled_runs(self) -> int:
+        """Pure-XY level runs add_frame tiled in the cascade launch itself."""
+        return int(lib().aqz_ds_stream_tiled_runs(self._h))
 
     def device_memory_usage(self) -> int:
         return lib().aqz_ds_device_memory_usage(self._h)

@@ -166,6 +166,7 @@ struct aqz_ds
     // $AQZ_STREAM_TILE_PASS=1: eager tiling as a tile pass behind the
     // row-major cascade (the round-2 path), for A/B
     bool tile_pass = false;
+    uint64_t stream_tiled_runs = 0; // runs the streaming path tiled in one launch
     // eager tiled readback (aqz_ds::eager): pinned copy of a level's tiles,
     // queued right behind its tile kernel, and which slot's frame it holds
     std::vector<uint8_t*> h_tiles;
@@ -439,6 +440,7 @@ launch_run_tiled(aqz_ds* ds, uint32_t L, uint32_t k, const void* cur,
     HIP_TRY(ds, e, "tiled cascade kernel");
     for (uint32_t j = 0; j < k; ++j)
         ds->tflag_slices[L + j][kk[j]] = slices[j];
+    ++ds->stream_tiled_runs;
     *launched = true;
     return AQZ_OK;
 }
@@ -2094,6 +2096,12 @@ int
 aqz_ds_last_batch_kind(const aqz_ds* ds)
 {
     return ds ? ds->last_batch_kind : -1;
+}
+
+uint64_t
+aqz_ds_stream_tiled_runs(const aqz_ds* ds)
+{
+    return ds ? ds->stream_tiled_runs : 0;
 }
 
 size_t

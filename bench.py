@@ -968,8 +968,92 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
         el = time.perf_counter() - t0
         res["tiled_take_ms_per_frame"] = round(el / n_frames * 1e3, 3)
         res["tile"] = list(tile)
+        res["tiled_one_pass_runs"] = ds.stream_tiled_runs()
+        res["async_overlap"] = measure_async_overlap(ds, geo, frames, n_frames, tile)
     ds.close()
     return res
+
+
+class HostTiler:
+    """Level 0 chunked on the host the way the patched
+    MultiscaleArray::write_frame has arrays_[0] do it while the GPU works
+    (Array::write_frame_to_chunks_, array.cpp:507-622: tile rows copied into
+    chunk-tile order, OpenMP over tiles): numpy copies of tile-row bands on
+    `threads` host threads (numpy releases the GIL inside the copy)."""
+
+    def __init__(self, H, W, dtype, tile, threads=16):
+        import concurrent.futures as cf
+        self.H, self.W = H, W
+        self.tr, self.tc = tile
+        self.nty, self.ntx = -(-H // self.tr), -(-W // self.tc)
+        self.buf = np.zeros((self.nty, self.ntx, self.tr, self.tc), dtype)
+        self.pool = cf.ThreadPoolExecutor(max_workers=threads)
+
+    def _band(self, frame, ty):
+        r0 = ty * self.tr
+        rows = min(self.tr, self.H - r0)
+        for tx in range(self.ntx):
+            c0 = tx * self.tc
+            cols = min(self.tc, self.W - c0)
+            self.buf[ty, tx, :rows, :cols] = frame[r0:r0 + rows, c0:c0 + cols]
+
+    def __call__(self, frame):
+        list(self.pool.map(lambda ty: self._band(frame, ty), range(self.nty)))
+        return self.buf
+
+    def close(self):
+        self.pool.shutdown()
+
+
+def measure_async_overlap(ds, geo, frames, n_frames, tile):
+    """SURVEY §8(f) row 1 as the patched MultiscaleArray::write_frame runs it
+    (acquire-zarr-hip.patch; multiscale.array.cpp:57-74,291-325): per frame,
+    add_frame_async (upload + pyramid + level tiling queued on the GPU), level
+    0 chunked on the host meanwhile, wait, then take_frame_tiled of every
+    level.  Beside it the same work in sequence (add_frame, then the host
+    tiling, then the takes) and the host tiling alone.  Every tile the takes
+    return for the last frame is compared bit for bit with the same frame
+    taken through the synchronous calls."""
+    W, H, _ = geo[0]
+    tiler = HostTiler(H, W, frames[0].dtype, tile)
+    n_lv = len(geo)
+
+    def takes():
+        return [ds.take_frame_tiled(L, tile[0], tile[1]) for L in range(1, n_lv)]
+
+    for i in range(3):  # warm
+        ds.add_frame_async(frames[i % 4])
+        tiler(frames[i % 4])
+        ds.wait()
+        takes()
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        ds.add_frame_async(frames[i % 4])
+        tiler(frames[i % 4])
+        ds.wait()
+        last_async = takes()
+    overlap = (time.perf_counter() - t0) / n_frames
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        ds.add_frame(frames[i % 4])
+        tiler(frames[i % 4])
+        last_sync = takes()
+    seq = (time.perf_counter() - t0) / n_frames
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        tiler(frames[i % 4])
+    host = (time.perf_counter() - t0) / n_frames
+    tiler.close()
+    # both loops end on frames[(n_frames - 1) % 4]
+    same = all(a is not None and b is not None and np.array_equal(a[0], b[0]) and
+               np.array_equal(a[1], b[1]) for a, b in zip(last_async, last_sync))
+    return {"async_overlap_ms_per_frame": round(overlap * 1e3, 3),
+            "sequential_ms_per_frame": round(seq * 1e3, 3),
+            "host_l0_tiling_ms_per_frame": round(host * 1e3, 3),
+            "host_threads": 16,
+            "async_equals_sync": bool(same),
+            "path": "add_frame_async; level 0 tiled on host threads; wait; "
+                    "take_frame_tiled(every level)"}
 
 
 def measure_e2e_sink(aqz, geo, dtype, method, n_frames, device, sink_dir):

@@ -477,6 +477,15 @@ int aqz_ds_run_host_batch(aqz_ds* ds,
  */
 int aqz_ds_last_batch_kind(const aqz_ds* ds);
 
+/*
+ * Diagnostic: how many runs of pure-XY levels the streaming path (add_frame)
+ * has written in ONE tiled-cascade launch — levels row-major into their
+ * slots and chunk-tiled, zero scan included, into the tiles
+ * aqz_ds_set_level_tiling asked for — instead of the cascade plus a tile pass
+ * per level ($AQZ_STREAM_TILE_PASS=1 forces the latter).
+ */
+uint64_t aqz_ds_stream_tiled_runs(const aqz_ds* ds);
+
 /* HIP ordinal the handle runs on (-1 for a null handle). */
 int aqz_ds_device(const aqz_ds* ds);
 

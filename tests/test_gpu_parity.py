@@ -441,19 +441,21 @@ TILE_CASES = [
 ]
 
 
-@pytest.mark.parametrize("eager", [False, True], ids=["on_demand", "eager"])
+@pytest.mark.parametrize("eager", ["on_demand", "eager", "eager_tile_pass"])
 @pytest.mark.parametrize("case", TILE_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{np.dtype(c[3]).name}")
-def test_take_frame_tiled(aqz, oracle, case, eager):
+def test_take_frame_tiled(aqz, oracle, case, eager, monkeypatch):
     """Chunk-tiled take (§8(f) row 2) equals the oracle's restatement of
     write_frame_to_chunks_ + write_tile_rows, zero scan included; some tiles
-    are forced all-zero."""
+    are forced all-zero.  `eager`: levels tiled in the cascade launch itself
+    (one pass), or by a tile pass behind it ($AQZ_STREAM_TILE_PASS=1)."""
     w, h, nl, dt, tr, tc = case
     geo = halving_geometry(w, h, nl)
     rng = np.random.default_rng(seed_of("tiled", w, h))
     frame = random_frames(rng, dt, (h, w), specials=False)
     frame[: h // 2, : w // 2] = 0  # zero tiles at every level
+    monkeypatch.setenv("AQZ_STREAM_TILE_PASS", "1" if eager == "eager_tile_pass" else "0")
     ds = aqz.Downsampler(geo, dt, 1)
-    if eager:  # tiles computed behind the pyramid (aqz_ds_set_level_tiling)
+    if eager != "on_demand":  # tiles computed behind the pyramid (aqz_ds_set_level_tiling)
         for L in range(1, nl):
             ds.set_level_tiling(L, tr, tc)
     ref = oracle.OracleDownsampler(geo, dt, 1)
@@ -467,6 +469,11 @@ def test_take_frame_tiled(aqz, oracle, case, eager):
         assert_parity(got[0], tiles, f"tiles L{L}")
         assert np.array_equal(got[1], nz), f"zero scan L{L}"
         assert ds.take_frame(L) is None  # the tiled take consumed the frame
+    if eager == "eager":
+        # every case here is one run of pure-XY levels: one tiled launch
+        assert ds.stream_tiled_runs() == 1
+    else:
+        assert ds.stream_tiled_runs() == 0
 
 
 def test_tile_frame_device_full_resolution(aqz, oracle):
@@ -562,11 +569,13 @@ def test_max_size_frame_two_fused_runs(aqz, oracle):
         assert_parity(from_device(outs[L], np.uint16, (h, w)), ref[L - 1], f"L{L}")
 
 
-def test_eager_tiling_follows_the_cached_frame(aqz, oracle):
+@pytest.mark.parametrize("tile_pass", ["0", "1"], ids=["one_pass", "tile_pass"])
+def test_eager_tiling_follows_the_cached_frame(aqz, oracle, tile_pass, monkeypatch):
     """With eager tiling on, the tiles always belong to the cached frame: an
     untaken frame keeps its tiles while newer frames are dropped, a plain
     take_frame consumes the frame, and a different tile shape falls back to
     on-demand tiling."""
+    monkeypatch.setenv("AQZ_STREAM_TILE_PASS", tile_pass)
     geo = halving_geometry(128, 96, 3)
     ds = aqz.Downsampler(geo, np.uint16, 1)
     ds.set_level_tiling(1, 16, 32)
@@ -584,6 +593,7 @@ def test_eager_tiling_follows_the_cached_frame(aqz, oracle):
     assert_parity(got[0], oracle.tile_frame(want2[0], 8, 8)[0], "L1 f2 on demand")
     assert np.array_equal(ds.take_frame(2), want1[1])  # plain take of f0
     assert ds.take_frame_tiled(2, 16, 16) is None
+    assert ds.stream_tiled_runs() == (3 if tile_pass == "0" else 0)
     ds.set_level_tiling(1, 0, 0)
 
 
@@ -627,6 +637,41 @@ def test_add_frame_async_matches_oracle(aqz, oracle, geo_kind):
         assert (a is None) == (b is None)
         if a is not None:
             assert_parity(a, b, f"back-to-back L{L}")
+    ds.close()
+
+
+@pytest.mark.parametrize("shape,tile", [((601, 1000), (64, 128)), ((4096, 4096), (256, 256)),
+                                        ((3000, 3000), (256, 256))],
+                         ids=["1000x601", "4096x4096", "3000x3000"])
+def test_add_frame_async_tiled_takes(aqz, oracle, shape, tile):
+    """The drop-in's streaming path as the patched MultiscaleArray::write_frame
+    runs it: every level tiled behind the pyramid (one tiled-cascade launch),
+    add_frame_async, then take_frame_tiled of every level — tiles and zero
+    scan equal to the oracle's, frame by frame, with untaken frames kept."""
+    H, W = shape
+    dims = [(aqz.TIME, 0, 1, 1), (aqz.SPACE, H, tile[0], 1), (aqz.SPACE, W, tile[1], 1)]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    assert len(geo) >= 3
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    for L in range(1, len(geo)):
+        ds.set_level_tiling(L, *tile)
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+    rng = np.random.default_rng(seed_of("async_tiled", H, W))
+    for i in range(3):
+        f = rng.integers(0, 65536, shape, dtype=np.uint16)
+        f[: H // 3, : W // 3] = 0  # zero tiles at every level
+        ds.add_frame_async(f)
+        ref.add_frame(f)
+        ds.wait()
+        for L in range(1, len(geo)):
+            if i == 1 and L == 2:
+                continue  # left untaken: frame 2 must not replace it
+            got = ds.take_frame_tiled(L, *tile)
+            want = ref.take_frame(L)
+            t, nz = oracle.tile_frame(want, *tile)
+            assert_parity(got[0], t, f"frame {i} L{L} tiles")
+            assert np.array_equal(got[1], nz), f"frame {i} L{L} zero scan"
+    assert ds.stream_tiled_runs() == 3 * -(-(len(geo) - 1) // 4)
     ds.close()
 
 
