@@ -836,6 +836,31 @@ stage_level(const StageCtx& sc,
             continue;
         T* d = reinterpret_cast<T*>(base) +
                uint64_t(rout0 + r - (band_row0 >> J)) * sc.stride[J - 1] + (cout0 - sc.scol[J - 1]);
+        // A lane's CO elements as one LDS vector write where they are whole
+        // and aligned (every row of an aligned band): element writes put the
+        // lanes 16 B apart for f32 level 1, a 4-way bank conflict (60% of
+        // LDS cycles, profiles/r03/f32/); the element path stays for edges
+        // and unaligned bands.
+        constexpr int VB = CO * int(sizeof(T));
+        if constexpr (VB == 16 || VB == 8 || VB == 4) {
+            if ((!EDGE || cout0 + CO <= wout) &&
+                (reinterpret_cast<uintptr_t>(d) & uintptr_t(VB - 1)) == 0) {
+                if constexpr (VB == 16) {
+                    u32x4 v;
+                    __builtin_memcpy(&v, out[r], 16);
+                    *reinterpret_cast<u32x4*>(d) = v;
+                } else if constexpr (VB == 8) {
+                    uint64_t v;
+                    __builtin_memcpy(&v, out[r], 8);
+                    *reinterpret_cast<uint64_t*>(d) = v;
+                } else {
+                    uint32_t v;
+                    __builtin_memcpy(&v, out[r], 4);
+                    *reinterpret_cast<uint32_t*>(d) = v;
+                }
+                continue;
+            }
+        }
 #pragma unroll
         for (int c = 0; c < CO; ++c) {
             if (!EDGE || cout0 + c < wout)

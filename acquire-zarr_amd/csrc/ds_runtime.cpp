@@ -281,10 +281,9 @@ reduce_slice_flags(const TileGeom& g, size_t slices, const uint8_t* flags,
                    uint8_t* tile_nonzero)
 {
     for (size_t t = 0; t < g.n_tiles; ++t) {
-        uint8_t any = 0;
-        for (size_t q = 0; q < slices; ++q)
-            any |= flags[t * slices + q];
-        tile_nonzero[t] = any ? 1 : 0;
+        // most tiles hold data: stop at the first set flag
+        const uint8_t* f = flags + t * slices;
+        tile_nonzero[t] = std::any_of(f, f + slices, [](uint8_t b) { return b != 0; }) ? 1 : 0;
     }
 }
 

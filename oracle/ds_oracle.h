@@ -9,8 +9,10 @@
  * Parity status: pinned by the reference's own known-answer tests
  * (tests/unit-tests/downsampler.cpp, downsampler-odd-z.cpp) and the pixel
  * expectations of python/tests/test_stream.py, restated as fixtures under
- * tests/golden/.  The reference itself is unbuildable in this image
- * (downsampler.hh includes nlohmann/json.hpp, which is absent), see DESIGN.md.
+ * tests/golden/; the chunk addressing by the 203 assertions of the
+ * reference's tests/unit-tests/array-dimensions-*.cpp.  The reference
+ * downsampler is not used as an oracle (downsampler.hh includes
+ * nlohmann/json.hpp, absent from this image), see DESIGN.md §3.
  */
 #ifndef DS_ORACLE_H
 #define DS_ORACLE_H

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round 3: F config (4096^2 f32) methods against their same-mix ceilings, the
+# 85 KiB staged band against the 64 KiB cap (direct stores), then counters
+# (wave stall buckets, LDS bank conflicts) per method and launch shape.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT=gpurun_out/r03_f32; mkdir -p $OUT
+export TMPDIR=/tmp
+for i in 1 2; do
+  for m in max min decimate mean; do
+    for e in "X=0" "AQZ_BAND_LDS_CAP=65536"; do
+      env $e timeout -k 10 120 python bench.py --workload 4096x4096_f32 --method $m --steps 20 --warmup 5 \
+        --cpu-seconds 0 --e2e-frames 0 --no-pmc > $OUT/ab.json 2> $OUT/ab.err || { tail -5 $OUT/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$OUT/ab.json'));r=d['roofline'];print('$m', '$e', r['avg_launch_us'], r['frac'], r['same_mix_ceiling']['frac_of_ceiling'], r['same_mix_ceiling']['GBps'], d['config']['check'])" | tee -a $OUT/f32_ab.log
+    done
+  done
+done
+run() { # tag env counters bench-args
+  local tag=$1 e=$2 c=$3; shift 3
+  env $e timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $OUT/$tag -o pmc -- \
+    python3 bench.py --pmc-child --steps 3 --warmup 1 "$@" > $OUT/$tag.log 2>&1 || { tail -5 $OUT/$tag.log; exit 1; }
+  python3 - "$OUT/$tag" "$tag" <<'PY' | tee -a $OUT/pmc_summary.txt
+import csv, glob, sys, collections
+f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
+acc = collections.defaultdict(list)
+for r in csv.DictReader(open(f)):
+    if "cascade" in r["Kernel_Name"]:
+        acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+print(sys.argv[2], {k: round(sum(v[1:]) / max(1, len(v) - 1)) for k, v in acc.items()})
+PY
+}
+C1="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES"
+C2="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAVES"
+C3="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY"
+for m in max mean; do
+  for e in "X=0" "AQZ_BAND_LDS_CAP=65536"; do
+    for c in "$C1" "$C2" "$C3"; do
+      tag="${m}_$(echo $e | tr -dc 'A-Z0-9')_$(echo $c | cut -c1-12 | tr -dc 'A-Z_')"
+      run "$tag" "$e" "$c" --workload 4096x4096_f32 --method $m
+    done
+  done
+done
+# streaming tiled take with the early-exit flag reduction
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-pmc --e2e-frames 48 \
+  > $OUT/bench_stream.json 2> $OUT/bench_stream.err || { tail -5 $OUT/bench_stream.err; exit 1; }
+python -c "import json;d=json.load(open('$OUT/bench_stream.json'));e=d['e2e'];print({k:e.get(k) for k in ('ms_per_frame','tiled_take_ms_per_frame','tiled_one_pass_runs')}, e['async_overlap'])"
+echo "== done"
