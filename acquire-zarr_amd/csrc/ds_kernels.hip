@@ -1043,9 +1043,28 @@ cascade_kernel(CascadeParams p)
 // is split into segments of seg_tiles tiles, one workgroup each, every level
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
+// Burst completion (complete != 0, whole bands only, no segments): no
+// barrier between the cascade and the stores.  Each wave stores, from LDS,
+// the 64-B bursts of its staged level rows that hold only its own bytes, and
+// for a burst it shares (with the neighbouring wave, or across a row end with
+// the first wave of the next row) it adds its byte count to the burst's LDS
+// counter: the wave that completes the count stores the whole burst.  Every
+// burst inside the band leaves in one piece, written once, and no wave waits
+// for another; only the band's first and last burst are partial.
+template<typename T>
+__device__ __forceinline__ void
+band_copy_chunks(const uint8_t* lds, uint8_t* g, uint32_t bytes, int lane)
+{
+    // both 16-B aligned, bytes a multiple of 64: 1 KiB per wave instruction
+    for (uint32_t q = uint32_t(lane); q < bytes / 16u; q += 64u) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(lds + 16u * q);
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(g + 16u * q));
+    }
+}
+
 template<typename T, int M, int NL, int C, bool NT = true>
 __global__ __launch_bounds__(512) void
-cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
+cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles, uint32_t complete)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t band_lds[];
     constexpr int R = 1 << NL;
@@ -1097,6 +1116,26 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         off += (sc.head[i] + len[i] + 15u) & ~15u;
     }
 
+    // burst completion counters, one per 64-B burst a staged level's band
+    // touches, cleared before any wave stages
+    uint32_t* cnt[kMaxFusedLevels] = {};
+    uint32_t base64[kMaxFusedLevels] = {};
+    if (complete) {
+        uint32_t words = 0;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            if (!((stage_mask >> i) & 1u))
+                continue;
+            base64[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 63u);
+            cnt[i] = reinterpret_cast<uint32_t*>(band_lds + off) + words;
+            words += (base64[i] + len[i] + 63u) / 64u;
+        }
+        uint32_t* c0 = reinterpret_cast<uint32_t*>(band_lds + off);
+        for (uint32_t k = threadIdx.x; k < words; k += blockDim.x)
+            c0[k] = 0;
+        __syncthreads();
+    }
+
     if (ux < p.units_x) { // wave-uniform
         const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
         const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
@@ -1104,6 +1143,64 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
             cascade_unit<T, M, NL, C, NT, false, true, true>(p, f, row0, col0, lane, &sc);
         else
             cascade_unit<T, M, NL, C, NT, true, true, true>(p, f, row0, col0, lane, &sc);
+    }
+
+    if (complete) {
+        if (ux >= p.units_x)
+            return;
+        // this wave's staged bytes are in LDS before any count says so
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        constexpr uint32_t b = uint32_t(sizeof(T));
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            if (!((stage_mask >> i) & 1u) || len[i] == 0)
+                continue;
+            const uint32_t wi = p.w[i];
+            const uint32_t cs = (ux * 64u * uint32_t(C)) >> (i + 1);
+            if (cs >= wi)
+                continue;
+            const uint32_t ce = min(cs + ((64u * uint32_t(C)) >> (i + 1)), wi);
+            const uint32_t b64 = base64[i];
+            // grid position x = byte offset from the 64-B boundary at or
+            // below the band's start; the band holds [b64, b64 + len)
+            const uint32_t band_end = b64 + len[i];
+            uint8_t* g = span[i] - b64;
+            const uint8_t* l = sc.lds[i] + sc.head[i] - b64; // l + x <-> g + x
+            for (uint32_t r = 0; r < rows_of[i]; ++r) {
+                const uint32_t fs = b64 + (r * wi + cs) * b;
+                const uint32_t fe = b64 + (r * wi + ce) * b;
+                const uint32_t k_in0 = (fs + 63u) >> 6, k_in1 = fe >> 6;
+                if (k_in1 > k_in0)
+                    band_copy_chunks<T>(l + 64u * k_in0, g + 64u * k_in0,
+                                        64u * (k_in1 - k_in0), lane);
+                const uint32_t kf = fs >> 6, kl = (fe - 1u) >> 6;
+                for (uint32_t k = kf; k <= kl; k += (kl > kf ? kl - kf : 1u)) {
+                    if (k >= k_in0 && k < k_in1)
+                        continue; // whole burst of this wave's own bytes
+                    const uint32_t lo = max(fs, 64u * k), hi = min(fe, 64u * k + 64u);
+                    const uint32_t blo = max(b64, 64u * k), bhi = min(band_end, 64u * k + 64u);
+                    uint32_t old = 0;
+                    if (lane == 0)
+                        old = atomicAdd(&cnt[i][k], hi - lo);
+                    old = __shfl(old, 0);
+                    if (old + (hi - lo) != bhi - blo)
+                        continue; // another wave's bytes are still missing
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (bhi - blo == 64u) {
+                        if (lane < 4) {
+                            const u32x4 v =
+                              *reinterpret_cast<const u32x4*>(l + 64u * k + 16u * uint32_t(lane));
+                            __builtin_nontemporal_store(
+                              v, reinterpret_cast<u32x4*>(g + 64u * k + 16u * uint32_t(lane)));
+                        }
+                    } else if (blo + uint32_t(lane) < bhi) {
+                        // the band's first or last burst: only its own bytes
+                        g[blo + uint32_t(lane)] = l[blo + uint32_t(lane)];
+                    }
+                }
+            }
+        }
+        return;
     }
     __syncthreads();
 
@@ -1166,7 +1263,7 @@ band_lds_cap()
 // bands; 0 if no level is staged).
 inline uint32_t
 band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
-               uint32_t seg_cols = 0)
+               uint32_t seg_cols = 0, bool complete = false)
 {
     uint64_t total = 0;
     for (int i = 0; i < n_out; ++i) {
@@ -1175,6 +1272,8 @@ band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
             const uint64_t w = seg_cols ? std::min<uint64_t>(seg_cols >> (i + 1), outs[i].w)
                                         : outs[i].w;
             total += (15 + rows * w * b + 15) & ~uint64_t(15);
+            if (complete) // burst completion counters
+                total += 4 * ((63 + rows * w * b + 63) / 64);
         }
     }
     return total > (1u << 30) ? (1u << 30) : uint32_t(total);
@@ -1916,6 +2015,11 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // 531 -> 516 us, 8192x2048 f32 1012 -> 962 us
         // (profiles/r02/band8/segments_ab.log); $AQZ_BAND_SEGMENTS=0: off.
         static const uint32_t band_force = uint32_t(int_env("AQZ_BAND_FORCE", 0));
+        // Misaligned bands of up to 8 tiles in burst-completion mode (no
+        // barrier: see cascade_band_kernel); $AQZ_BAND_COMPLETE=0: the
+        // barrier form for bands of <= 4 tiles and direct stores above.
+        static const bool band_complete = int_env("AQZ_BAND_COMPLETE", 1) != 0;
+        bool complete = false;
         static const bool band_aligned = int_env("AQZ_BAND_ALIGNED", 1) != 0;
         static const bool band_segments = int_env("AQZ_BAND_SEGMENTS", 1) != 0;
         uint32_t band_waves = p.units_x;
@@ -1923,6 +2027,11 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         uint32_t wide_max = 4, seg_tiles = 0;
         if (band_force) {
             stage_mask |= band_force & all_levels;
+            wide_max = 8;
+        } else if (band_complete && stage_mask && band_waves <= 8 &&
+                   band_lds_bytes(sizeof(T), outs, n_out, stage_mask, 0, true) <=
+                     band_lds_cap()) {
+            complete = true;
             wide_max = 8;
         } else if (band_aligned && stage_mask == 0 && band_waves >= 5 && band_waves <= 8 &&
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
@@ -1937,7 +2046,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             wide_max = 8;
         }
         const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask,
-                                            seg_tiles * 64u * cols);
+                                            seg_tiles * 64u * cols, complete);
         const bool band = stage_mask && !band_off &&
                           band_waves <= wide_max && lds <= band_lds_cap() &&
                           total < (1ull << 31);
@@ -1957,7 +2066,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
+                                               lds, stream, p, stage_mask, seg_tiles,
+                                               uint32_t(complete));
                             break;
                         case 2:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -1965,7 +2075,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
+                                               lds, stream, p, stage_mask, seg_tiles,
+                                               uint32_t(complete));
                             break;
                         case 3:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -1973,7 +2084,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
+                                               lds, stream, p, stage_mask, seg_tiles,
+                                               uint32_t(complete));
                             break;
                         default:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -1981,7 +2093,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
+                                               lds, stream, p, stage_mask, seg_tiles,
+                                               uint32_t(complete));
                             break;
                     }
                     return;

@@ -970,6 +970,7 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
         res["tile"] = list(tile)
         res["tiled_one_pass_runs"] = ds.stream_tiled_runs()
         res["async_overlap"] = measure_async_overlap(ds, geo, frames, n_frames, tile)
+        res["async_overlap_ms_per_frame"] = res["async_overlap"]["async_overlap_ms_per_frame"]
     ds.close()
     return res
 
