@@ -371,6 +371,7 @@ struct CascadeParams
     uint32_t remap;                  // 1: XCD-contiguous block order (cascade_kernel)
     uint32_t wb;                     // bit J-1: level J's row-major stores write-back, not nt
     uint32_t order;                  // unit order: 0 columns fastest, 1 frames, 2 row bands
+    uint32_t seg_w;                  // > 0: a workgroup is seg_w column tiles of one row band
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
 };
 
@@ -998,11 +999,20 @@ cascade_kernel(CascadeParams p)
         if (blk < nb8)
             blk = (blk & 7u) * (nb8 >> 3) + (blk >> 3);
     }
-    const uint32_t u = blk * (blockDim.x >> 6) + wave;
-    if (u >= p.total_units)
-        return;
     uint32_t ux, uy, f;
-    if (TILED || p.order == 0) {
+    if (!TILED && p.seg_w) {
+        // band-aligned workgroups: the waves that share a row's partial
+        // 64-B bursts run on one CU, so the halves meet in its L2
+        const uint32_t segs = (p.units_x + p.seg_w - 1) / p.seg_w;
+        const uint32_t band = blk / segs;
+        ux = (blk - band * segs) * p.seg_w + wave;
+        if (ux >= p.units_x || band >= p.total_units / p.units_x)
+            return;
+        uy = band % p.units_y;
+        f = band / p.units_y;
+    } else if (const uint32_t u = blk * (blockDim.x >> 6) + wave; u >= p.total_units) {
+        return;
+    } else if (TILED || p.order == 0) {
         ux = u % p.units_x;
         const uint32_t t = u / p.units_x;
         uy = t % p.units_y;
@@ -1043,28 +1053,9 @@ cascade_kernel(CascadeParams p)
 // is split into segments of seg_tiles tiles, one workgroup each, every level
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
-// Burst completion (complete != 0, whole bands only, no segments): no
-// barrier between the cascade and the stores.  Each wave stores, from LDS,
-// the 64-B bursts of its staged level rows that hold only its own bytes, and
-// for a burst it shares (with the neighbouring wave, or across a row end with
-// the first wave of the next row) it adds its byte count to the burst's LDS
-// counter: the wave that completes the count stores the whole burst.  Every
-// burst inside the band leaves in one piece, written once, and no wave waits
-// for another; only the band's first and last burst are partial.
-template<typename T>
-__device__ __forceinline__ void
-band_copy_chunks(const uint8_t* lds, uint8_t* g, uint32_t bytes, int lane)
-{
-    // both 16-B aligned, bytes a multiple of 64: 1 KiB per wave instruction
-    for (uint32_t q = uint32_t(lane); q < bytes / 16u; q += 64u) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(lds + 16u * q);
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(g + 16u * q));
-    }
-}
-
 template<typename T, int M, int NL, int C, bool NT = true>
 __global__ __launch_bounds__(512) void
-cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles, uint32_t complete)
+cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t band_lds[];
     constexpr int R = 1 << NL;
@@ -1116,26 +1107,6 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles, ui
         off += (sc.head[i] + len[i] + 15u) & ~15u;
     }
 
-    // burst completion counters, one per 64-B burst a staged level's band
-    // touches, cleared before any wave stages
-    uint32_t* cnt[kMaxFusedLevels] = {};
-    uint32_t base64[kMaxFusedLevels] = {};
-    if (complete) {
-        uint32_t words = 0;
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            if (!((stage_mask >> i) & 1u))
-                continue;
-            base64[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 63u);
-            cnt[i] = reinterpret_cast<uint32_t*>(band_lds + off) + words;
-            words += (base64[i] + len[i] + 63u) / 64u;
-        }
-        uint32_t* c0 = reinterpret_cast<uint32_t*>(band_lds + off);
-        for (uint32_t k = threadIdx.x; k < words; k += blockDim.x)
-            c0[k] = 0;
-        __syncthreads();
-    }
-
     if (ux < p.units_x) { // wave-uniform
         const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
         const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
@@ -1143,64 +1114,6 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles, ui
             cascade_unit<T, M, NL, C, NT, false, true, true>(p, f, row0, col0, lane, &sc);
         else
             cascade_unit<T, M, NL, C, NT, true, true, true>(p, f, row0, col0, lane, &sc);
-    }
-
-    if (complete) {
-        if (ux >= p.units_x)
-            return;
-        // this wave's staged bytes are in LDS before any count says so
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        constexpr uint32_t b = uint32_t(sizeof(T));
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            if (!((stage_mask >> i) & 1u) || len[i] == 0)
-                continue;
-            const uint32_t wi = p.w[i];
-            const uint32_t cs = (ux * 64u * uint32_t(C)) >> (i + 1);
-            if (cs >= wi)
-                continue;
-            const uint32_t ce = min(cs + ((64u * uint32_t(C)) >> (i + 1)), wi);
-            const uint32_t b64 = base64[i];
-            // grid position x = byte offset from the 64-B boundary at or
-            // below the band's start; the band holds [b64, b64 + len)
-            const uint32_t band_end = b64 + len[i];
-            uint8_t* g = span[i] - b64;
-            const uint8_t* l = sc.lds[i] + sc.head[i] - b64; // l + x <-> g + x
-            for (uint32_t r = 0; r < rows_of[i]; ++r) {
-                const uint32_t fs = b64 + (r * wi + cs) * b;
-                const uint32_t fe = b64 + (r * wi + ce) * b;
-                const uint32_t k_in0 = (fs + 63u) >> 6, k_in1 = fe >> 6;
-                if (k_in1 > k_in0)
-                    band_copy_chunks<T>(l + 64u * k_in0, g + 64u * k_in0,
-                                        64u * (k_in1 - k_in0), lane);
-                const uint32_t kf = fs >> 6, kl = (fe - 1u) >> 6;
-                for (uint32_t k = kf; k <= kl; k += (kl > kf ? kl - kf : 1u)) {
-                    if (k >= k_in0 && k < k_in1)
-                        continue; // whole burst of this wave's own bytes
-                    const uint32_t lo = max(fs, 64u * k), hi = min(fe, 64u * k + 64u);
-                    const uint32_t blo = max(b64, 64u * k), bhi = min(band_end, 64u * k + 64u);
-                    uint32_t old = 0;
-                    if (lane == 0)
-                        old = atomicAdd(&cnt[i][k], hi - lo);
-                    old = __shfl(old, 0);
-                    if (old + (hi - lo) != bhi - blo)
-                        continue; // another wave's bytes are still missing
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    if (bhi - blo == 64u) {
-                        if (lane < 4) {
-                            const u32x4 v =
-                              *reinterpret_cast<const u32x4*>(l + 64u * k + 16u * uint32_t(lane));
-                            __builtin_nontemporal_store(
-                              v, reinterpret_cast<u32x4*>(g + 64u * k + 16u * uint32_t(lane)));
-                        }
-                    } else if (blo + uint32_t(lane) < bhi) {
-                        // the band's first or last burst: only its own bytes
-                        g[blo + uint32_t(lane)] = l[blo + uint32_t(lane)];
-                    }
-                }
-            }
-        }
-        return;
     }
     __syncthreads();
 
@@ -1263,7 +1176,7 @@ band_lds_cap()
 // bands; 0 if no level is staged).
 inline uint32_t
 band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
-               uint32_t seg_cols = 0, bool complete = false)
+               uint32_t seg_cols = 0)
 {
     uint64_t total = 0;
     for (int i = 0; i < n_out; ++i) {
@@ -1272,8 +1185,6 @@ band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
             const uint64_t w = seg_cols ? std::min<uint64_t>(seg_cols >> (i + 1), outs[i].w)
                                         : outs[i].w;
             total += (15 + rows * w * b + 15) & ~uint64_t(15);
-            if (complete) // burst completion counters
-                total += 4 * ((63 + rows * w * b + 63) / 64);
         }
     }
     return total > (1u << 30) ? (1u << 30) : uint32_t(total);
@@ -2015,11 +1926,6 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // 531 -> 516 us, 8192x2048 f32 1012 -> 962 us
         // (profiles/r02/band8/segments_ab.log); $AQZ_BAND_SEGMENTS=0: off.
         static const uint32_t band_force = uint32_t(int_env("AQZ_BAND_FORCE", 0));
-        // Misaligned bands of up to 8 tiles in burst-completion mode (no
-        // barrier: see cascade_band_kernel); $AQZ_BAND_COMPLETE=0: the
-        // barrier form for bands of <= 4 tiles and direct stores above.
-        static const bool band_complete = int_env("AQZ_BAND_COMPLETE", 1) != 0;
-        bool complete = false;
         static const bool band_aligned = int_env("AQZ_BAND_ALIGNED", 1) != 0;
         static const bool band_segments = int_env("AQZ_BAND_SEGMENTS", 1) != 0;
         uint32_t band_waves = p.units_x;
@@ -2027,11 +1933,6 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         uint32_t wide_max = 4, seg_tiles = 0;
         if (band_force) {
             stage_mask |= band_force & all_levels;
-            wide_max = 8;
-        } else if (band_complete && stage_mask && band_waves <= 8 &&
-                   band_lds_bytes(sizeof(T), outs, n_out, stage_mask, 0, true) <=
-                     band_lds_cap()) {
-            complete = true;
             wide_max = 8;
         } else if (band_aligned && stage_mask == 0 && band_waves >= 5 && band_waves <= 8 &&
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
@@ -2046,12 +1947,28 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             wide_max = 8;
         }
         const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask,
-                                            seg_tiles * 64u * cols, complete);
+                                            seg_tiles * 64u * cols);
         const bool band = stage_mask && !band_off &&
                           band_waves <= wide_max && lds <= band_lds_cap() &&
                           total < (1ull << 31);
         const uint32_t segs = seg_tiles ? (p.units_x + seg_tiles - 1) / seg_tiles : 1u;
         const uint32_t bands = p.units_y * n_frames * segs;
+        // Direct stores of rows that split 64-B bursts, bands wider than the
+        // barrier form takes: one workgroup per band (or per balanced piece
+        // of <= 8 tiles), so a burst shared by neighbouring waves is written
+        // through one L2.  3000^2 622 -> 576 us, 2600^2 601 -> 540 us,
+        // 5472x3648 571 -> 540 us against 4-wave blocks that straddle bands
+        // (profiles/r03/misaligned/); $AQZ_BAND_WG=0: off.
+        static const bool band_wg = int_env("AQZ_BAND_WG", 1) != 0;
+        uint32_t wpb_run = wpb;
+        uint32_t grid_run = grid;
+        if (!band && band_wg && stage_mask && !band_force && p.order == 0 && p.units_x > 4) {
+            const uint32_t nseg = (p.units_x + 7) / 8;
+            p.seg_w = (p.units_x + nseg - 1) / nseg;
+            wpb_run = p.seg_w;
+            grid_run = nseg * p.units_y * n_frames;
+            p.main_blocks = grid_run;
+        }
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
             auto go = [&](auto ctag, auto nttag) {
@@ -2066,8 +1983,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles,
-                                               uint32_t(complete));
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                         case 2:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -2075,8 +1991,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles,
-                                               uint32_t(complete));
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                         case 3:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -2084,8 +1999,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles,
-                                               uint32_t(complete));
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                         default:
                             if (lds > 65536) // above the default per-workgroup LDS
@@ -2093,27 +2007,26 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                                   reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C, NT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
                             hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles,
-                                               uint32_t(complete));
+                                               lds, stream, p, stage_mask, seg_tiles);
                             break;
                     }
                     return;
                 }
                 switch (n_out) {
                     case 1:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT>), dim3(grid), dim3(64 * wpb),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT>), dim3(grid_run), dim3(64 * wpb_run),
                                            0, stream, p);
                         break;
                     case 2:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT>), dim3(grid), dim3(64 * wpb),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT>), dim3(grid_run), dim3(64 * wpb_run),
                                            0, stream, p);
                         break;
                     case 3:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT>), dim3(grid), dim3(64 * wpb),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT>), dim3(grid_run), dim3(64 * wpb_run),
                                            0, stream, p);
                         break;
                     default:
-                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT>), dim3(grid), dim3(64 * wpb),
+                        hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT>), dim3(grid_run), dim3(64 * wpb_run),
                                            0, stream, p);
                         break;
                 }
