@@ -84,25 +84,42 @@ def aggregate_gpix(world: int, frames_per_rank: int, W: int, H: int, steps: int,
     return world * frames_per_rank * W * H * steps / elapsed_max / 1e9
 
 
+def grouped_p2p(dist, ops):
+    """One grouped point-to-point batch: `ops` = [("send"|"recv", tensor,
+    peer)].  Under nccl (RCCL) it is dist.batch_isend_irecv — ncclGroupStart,
+    every send/recv, ncclGroupEnd — so all peers' xGMI links stream at once.
+    gloo moves host memory only: device tensors are staged through host
+    copies there (the one-GPU rehearsal of the N-rank path)."""
+    if not ops:
+        return
+    staged = []
+    p2p = []
+    host = dist.get_backend() != "nccl"
+    for kind, t, peer in ops:
+        if host and t.is_cuda:
+            h = t.cpu() if kind == "send" else t.new_empty(t.shape, device="cpu")
+            if kind == "recv":
+                staged.append((t, h))
+            t = h
+        p2p.append(dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer))
+    for q in dist.batch_isend_irecv(p2p):
+        q.wait()
+    for dev, h in staged:
+        dev.copy_(h)
+
+
 def scatter_frames(pool, local, frame_bytes: int, frames_per_rank: int, dist,
                    rank: int, world: int):
     """Batched-frame config F over xGMI: rank 0 holds every
     rank's frames contiguously in `pool` (rank r's block at r*frames_per_rank)
     and sends each block to its rank as ONE grouped point-to-point batch
-    (dist.batch_isend_irecv: ncclGroupStart / ncclSend x N / ncclGroupEnd
-    under RCCL, so every peer's xGMI link streams at once).  Returns the
-    tensor this rank computes on."""
+    (grouped_p2p).  Returns the tensor this rank computes on."""
     blk = frames_per_rank * frame_bytes
     if rank == 0:
-        ops = [dist.P2POp(dist.isend, pool[r * blk:(r + 1) * blk], r) for r in range(1, world)]
-        mine = pool[:blk]
-    else:
-        ops = [dist.P2POp(dist.irecv, local[:blk], 0)]
-        mine = local[:blk]
-    if ops:
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
-    return mine
+        grouped_p2p(dist, [("send", pool[r * blk:(r + 1) * blk], r) for r in range(1, world)])
+        return pool[:blk]
+    grouped_p2p(dist, [("recv", local[:blk], 0)])
+    return local[:blk]
 
 
 def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
@@ -119,13 +136,10 @@ def gather_levels(level_bufs, pool_levels, dist, rank: int, world: int):
         n = buf.numel()
         if rank == 0:
             pool_levels[L][:n].copy_(buf)
-            ops += [dist.P2POp(dist.irecv, pool_levels[L][r * n:(r + 1) * n], r)
-                    for r in range(1, world)]
+            ops += [("recv", pool_levels[L][r * n:(r + 1) * n], r) for r in range(1, world)]
         else:
-            ops.append(dist.P2POp(dist.isend, buf, 0))
-    if ops:
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
+            ops.append(("send", buf, 0))
+    grouped_p2p(dist, ops)
 
 
 def resequence(per_rank_frames, world: int):

@@ -154,7 +154,9 @@ def test_scatter_gather_are_grouped():
     import inspect
     sys.path.insert(0, ROOT)
     import bench
+    src = inspect.getsource(bench.grouped_p2p)
+    assert "batch_isend_irecv" in src and "P2POp" in src
     for fn in (bench.scatter_frames, bench.gather_levels):
         src = inspect.getsource(fn)
-        assert "batch_isend_irecv" in src and "P2POp" in src
+        assert "grouped_p2p(" in src
         assert "dist.isend(" not in src and "dist.irecv(" not in src
