@@ -36,7 +36,7 @@ EXPORTS = (
     "aqz_ds_last_batch_kind", "aqz_ds_stream_tiled_runs", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
     "aqz_ds_run_device_batch_tiled", "aqz_ds_tiled_flag_slots",
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
-    "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_set_input_transpose",
+    "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_add_frame_async_take", "aqz_ds_set_input_transpose",
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
     "aqz_blosc_filter_device", "aqz_crc32c_device", "aqz_tile_slices",
     "aqz_tile_frame_device_sliced",
@@ -68,6 +68,16 @@ class LevelDesc(ctypes.Structure):
     _fields_ = [("width", ctypes.c_uint32),
                 ("height", ctypes.c_uint32),
                 ("planes", ctypes.c_uint32)]
+
+
+TAKE_NONE, TAKE_INTO, TAKE_HOLD = 0, 1, 2
+
+
+class LevelTake(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("tile_rows", ctypes.c_uint32),
+                ("tile_cols", ctypes.c_uint32), ("dst", ctypes.c_void_p),
+                ("cap", ctypes.c_size_t), ("tile_nonzero", ctypes.c_void_p),
+                ("nbytes", ctypes.c_size_t), ("has_frame", ctypes.c_int)]
 
 
 class ChunkLattice(ctypes.Structure):
@@ -115,6 +125,7 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_destroy.restype = None
     L.aqz_ds_add_frame.argtypes = [vp, vp, sz]
     L.aqz_ds_add_frame_async.argtypes = [vp, vp, sz]
+    L.aqz_ds_add_frame_async_take.argtypes = [vp, vp, sz, ctypes.POINTER(LevelTake)]
     L.aqz_ds_wait.argtypes = [vp]
     L.aqz_ds_set_input_transpose.argtypes = [vp, ctypes.c_int]
     L.aqz_ds_take_input_frame.argtypes = [vp, u32, u32, vp, sz, vp, ctypes.POINTER(sz),
@@ -258,6 +269,7 @@ class Downsampler:
         self._h = h
         self.method = method
         self._pending = None  # frame of a pending add_frame_async
+        self._takes = None    # (LevelTake array, buffers) of add_frame_async_take
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -374,6 +386,59 @@ class Downsampler:
             self._check(lib().aqz_ds_wait(self._h))
         finally:
             self._pending = None
+
+    def add_frame_async_take(self, frame: np.ndarray, tiles, hold=()):
+        """aqz_ds_add_frame_async_take: every level L >= 1 taken in the
+        background job right behind the add — chunk-tiled when tiles[L] =
+        (tile_rows, tile_cols), row-major when tiles[L] is None — except the
+        levels in `hold` (AQZ_TAKE_HOLD).  wait_takes() returns the results."""
+        frame = np.ascontiguousarray(frame)
+        if frame.dtype != self.dtype:
+            raise TypeError(f"frame dtype {frame.dtype} != {self.dtype}")
+        n = self.n_levels
+        arr = (LevelTake * n)()
+        bufs = [None] * n
+        for L in range(1, n):
+            w, h, _ = self.geometry[L]
+            if L in hold:
+                arr[L].mode = TAKE_HOLD
+                continue
+            t = tiles[L] if tiles is not None else None
+            if t:
+                tr, tc = t
+                nt = (-(-h // tr)) * (-(-w // tc))
+                out = np.empty((nt, tr, tc), dtype=self.dtype)
+                nz = np.empty(nt, dtype=np.uint8)
+                arr[L] = LevelTake(TAKE_INTO, tr, tc, out.ctypes.data, out.nbytes,
+                                   nz.ctypes.data, 0, 0)
+                bufs[L] = (out, nz)
+            else:
+                out = np.empty((h, w), dtype=self.dtype)
+                arr[L] = LevelTake(TAKE_INTO, 0, 0, out.ctypes.data, out.nbytes, None, 0, 0)
+                bufs[L] = (out, None)
+        prev, self._pending = self._pending, frame
+        try:
+            self._check(lib().aqz_ds_add_frame_async_take(self._h, frame.ctypes.data,
+                                                          frame.nbytes, arr))
+            self._takes = (arr, bufs)
+        finally:
+            del prev
+
+    def wait_takes(self):
+        """Wait for add_frame_async_take; per level None (no frame, or held),
+        a row-major (h, w) array, or (tiles, zero-scan bools)."""
+        arr, bufs = self._takes
+        try:
+            self.wait()
+        finally:
+            self._takes = None
+        out = [None] * self.n_levels
+        for L in range(1, self.n_levels):
+            if arr[L].mode != TAKE_INTO or not arr[L].has_frame:
+                continue
+            a, nz = bufs[L]
+            out[L] = a if nz is None else (a, nz.astype(bool))
+        return out
 
     def add_device_frame(self, device_ptr: int, nbytes: int):
         self._check(lib().aqz_ds_add_device_frame(self._h, device_ptr, nbytes))

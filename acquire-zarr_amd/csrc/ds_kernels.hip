@@ -1938,6 +1938,14 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
             stage_mask = all_levels;
             wide_max = 8;
+            // $AQZ_BAND_SEG4=1 (A/B): 4-tile segments, so that a band whose
+            // LDS leaves room for one workgroup per CU (4096 f32: 85 KiB)
+            // runs two or three, overlapping one's stores with another's loads
+            static const int seg4 = int_env("AQZ_BAND_SEG4", 0);
+            if (seg4 == 1) {
+                seg_tiles = 4;
+                band_waves = 4;
+            }
         } else if (band_aligned && band_segments && stage_mask == 0 && band_waves > 8 &&
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels, 8u * 64u * cols) <=
                      band_lds_cap()) {

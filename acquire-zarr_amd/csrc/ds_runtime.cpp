@@ -107,6 +107,10 @@ struct aqz_ds
     std::vector<uint8_t> zh;        // level L halves Z (L >= 1)
     std::vector<uint32_t> count;    // level_frame_count_
     std::vector<uint8_t> has_partial;
+    // aqz_ds_add_frame_async_take with AQZ_TAKE_HOLD: the caller still holds
+    // an untaken frame of the level, so new ones are dropped (the emplace
+    // rule, downsampler.cpp:599-605) as if it were cached here
+    std::vector<uint8_t> held;
 
     hipStream_t stream = nullptr;
     void* d_in = nullptr;                      // level-0 frame on device
@@ -200,6 +204,7 @@ struct aqz_ds
         std::mutex m;
         std::condition_variable cv;
         const void* frame = nullptr; // the pending job's frame, null when idle
+        aqz_level_take* takes = nullptr; // aqz_ds_add_frame_async_take's takes
         bool stop = false;
         int rc = 0;                  // status of the last finished job
     } async;
@@ -361,7 +366,7 @@ emit(aqz_ds* ds, uint32_t level, const void* d_frame, const Sink& sink, bool pre
     }
     // unordered_map::emplace keeps an untaken frame; the new one is dropped
     // (it stays in the free slot only as the next level's input).
-    if (ds->cached[level] < 0) {
+    if (ds->cached[level] < 0 && !ds->held[level]) {
         const int k = (want == ds->slot[level].first) ? 0 : 1;
         ds->cached[level] = k;
         const auto [tr, tc] = ds->tiling[level];
@@ -677,6 +682,121 @@ add_host_frame(aqz_ds* ds, const void* host_frame)
     return AQZ_OK;
 }
 
+// aqz_ds_take_frame's body (its caller has settled any pending add).
+int
+take_plain(aqz_ds* ds, uint32_t level, void* dst, size_t cap, size_t* nbytes, int* has_frame)
+{
+    *has_frame = 0;
+    if (level == 0 || level >= ds->n)
+        return AQZ_OK; // the reference's map lookup simply misses
+    if (ds->cached[level] < 0)
+        return AQZ_OK;
+    *has_frame = 1;
+    if (nbytes)
+        *nbytes = ds->bytes[level];
+    if (!dst)
+        return AQZ_OK;
+    if (cap < ds->bytes[level])
+        return ds->fail_arg("take_frame: buffer too small");
+    if (int rc = bind_device(ds))
+        return rc;
+    if (ds->eager && ds->host_for[level] == ds->cached[level]) {
+        // already on its way to pinned memory (eager_readback)
+        HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
+        std::memcpy(dst, ds->h_level[level], ds->bytes[level]);
+    } else {
+        // HBM -> caller memory directly (stream-ordered after the kernels)
+        HIP_TRY(ds,
+                hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
+                               ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
+                "hipMemcpyAsync D2H");
+        HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
+    }
+    ds->cached[level] = -1;
+    ds->tiled_for[level] = -1;
+    ds->host_for[level] = -1;
+    ds->htile_for[level] = -1;
+    return AQZ_OK;
+}
+
+// aqz_ds_take_frame_tiled's body (its caller has settled any pending add).
+int
+take_tiled(aqz_ds* ds,
+           uint32_t level,
+           uint32_t tile_rows,
+           uint32_t tile_cols,
+           void* dst,
+           size_t cap,
+           uint8_t* tile_nonzero,
+           size_t* nbytes,
+           int* has_frame)
+{
+    *has_frame = 0;
+    if (tile_rows == 0 || tile_cols == 0)
+        return ds->fail_arg("take_frame_tiled: empty tile");
+    if (level == 0 || level >= ds->n || ds->cached[level] < 0)
+        return AQZ_OK;
+    const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
+    *has_frame = 1;
+    if (nbytes)
+        *nbytes = g.tile_bytes;
+    if (!dst)
+        return AQZ_OK;
+    if (cap < g.tile_bytes)
+        return ds->fail_arg("take_frame_tiled: buffer too small");
+    if (int rc = bind_device(ds))
+        return rc;
+    const int k = ds->cached[level];
+    if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
+        ds->tiled_for[level] == k && ds->htile_for[level] == k) {
+        // tiled and copied out when the frame was emitted (eager readback)
+        HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
+        std::memcpy(dst, ds->h_tiles[level], g.tile_bytes);
+        if (tile_nonzero)
+            reduce_slice_flags(g, ds->tflag_slices[level][k],
+                               k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
+                               tile_nonzero);
+    } else if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
+               ds->tiled_for[level] == k) {
+        // tiled when the frame was emitted (aqz_ds_set_level_tiling)
+        if (int rc = tiles_to_host(ds, g, ds->tflag_slices[level][k],
+                                   k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
+                                   k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
+                                   dst, tile_nonzero))
+            return rc;
+    } else if (int rc = tile_to_host(ds, ds->slot_ptr(level, k), ds->lv[level], tile_rows,
+                                     tile_cols, g, dst, tile_nonzero)) {
+        return rc;
+    }
+    ds->cached[level] = -1;
+    ds->tiled_for[level] = -1;
+    ds->host_for[level] = -1;
+    ds->htile_for[level] = -1;
+    ds->no_eager[level] = 1; // this caller takes the level tiled
+    return AQZ_OK;
+}
+
+// The takes of aqz_ds_add_frame_async_take, in the job right behind its add:
+// each level's device-to-host copy then overlaps the caller's work too.
+int
+run_takes(aqz_ds* ds, aqz_level_take* takes)
+{
+    for (uint32_t L = 1; L < ds->n; ++L) {
+        aqz_level_take& t = takes[L];
+        t.has_frame = 0;
+        t.nbytes = 0;
+        if (t.mode != AQZ_TAKE_INTO)
+            continue;
+        const int rc = (t.tile_rows || t.tile_cols)
+                         ? take_tiled(ds, L, t.tile_rows, t.tile_cols, t.dst, t.cap,
+                                      t.tile_nonzero, &t.nbytes, &t.has_frame)
+                         : take_plain(ds, L, t.dst, t.cap, &t.nbytes, &t.has_frame);
+        if (rc)
+            return rc;
+    }
+    return AQZ_OK;
+}
+
 void
 async_worker(aqz_ds* ds)
 {
@@ -687,16 +807,20 @@ async_worker(aqz_ds* ds)
         if (!a.frame)
             return; // stop requested and nothing pending
         const void* frame = a.frame;
+        aqz_level_take* takes = a.takes;
         lk.unlock();
         int rc;
         try {
             rc = add_host_frame(ds, frame);
+            if (rc == AQZ_OK && takes)
+                rc = run_takes(ds, takes);
         } catch (...) {
             rc = ABI_GUARD_FAIL(ds); // reported by the next settle()
         }
         lk.lock();
         a.rc = rc;
         a.frame = nullptr;
+        a.takes = nullptr;
         a.cv.notify_all();
     }
 }
@@ -1021,6 +1145,7 @@ aqz_ds_create(const aqz_level_desc* levels,
         ds->staged = env_flag("AQZ_PINNED_STAGING");
         ds->tiling.assign(n_levels, { 0, 0 });
         ds->tslot.assign(n_levels, { nullptr, nullptr });
+        ds->held.assign(n_levels, 0);
         ds->tflags.assign(n_levels, { nullptr, nullptr });
         ds->tflag_cap.assign(n_levels, { 0, 0 });
         ds->tflag_slices.assign(n_levels, { 1, 1 });
@@ -1116,6 +1241,7 @@ aqz_ds_add_frame(aqz_ds* ds, const void* host_frame, size_t nbytes)
             return rc;
         if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame"))
             return rc;
+        std::fill(ds->held.begin(), ds->held.end(), 0);
         return add_host_frame(ds, host_frame);
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
@@ -1132,12 +1258,53 @@ aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes)
             return rc;
         if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame_async"))
             return rc;
+        std::fill(ds->held.begin(), ds->held.end(), 0);
         auto& a = ds->async;
         if (!a.worker.joinable())
             a.worker = std::thread(async_worker, ds);
         {
             std::lock_guard<std::mutex> lk(a.m);
             a.frame = host_frame;
+        }
+        a.cv.notify_all();
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
+}
+
+int
+aqz_ds_add_frame_async_take(aqz_ds* ds,
+                            const void* host_frame,
+                            size_t nbytes,
+                            aqz_level_take* takes)
+{
+    try {
+        if (!ds || !takes)
+            return AQZ_INVALID_ARGUMENT;
+        if (int rc = settle(ds))
+            return rc;
+        if (int rc = check_host_frame(ds, host_frame, nbytes, "add_frame_async_take"))
+            return rc;
+        for (uint32_t L = 1; L < ds->n; ++L) {
+            const aqz_level_take& t = takes[L];
+            if (t.mode < AQZ_TAKE_NONE || t.mode > AQZ_TAKE_HOLD ||
+                ((t.tile_rows == 0) != (t.tile_cols == 0)))
+                return ds->fail_arg("add_frame_async_take: level " + std::to_string(L) +
+                                    ": bad mode or tile shape");
+            if (t.mode == AQZ_TAKE_HOLD && ds->cached[L] >= 0)
+                return ds->fail_arg("add_frame_async_take: level " + std::to_string(L) +
+                                    " is held by the caller but also cached here");
+        }
+        for (uint32_t L = 1; L < ds->n; ++L)
+            ds->held[L] = takes[L].mode == AQZ_TAKE_HOLD;
+        auto& a = ds->async;
+        if (!a.worker.joinable())
+            a.worker = std::thread(async_worker, ds);
+        {
+            std::lock_guard<std::mutex> lk(a.m);
+            a.frame = host_frame;
+            a.takes = takes;
         }
         a.cv.notify_all();
         return AQZ_OK;
@@ -1170,6 +1337,7 @@ aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes)
             return ds->fail_arg("add_device_frame: expected " +
                                 std::to_string(ds->bytes[0]) + " bytes, got " +
                                 std::to_string(nbytes));
+        std::fill(ds->held.begin(), ds->held.end(), 0);
         if (int rc = bind_device(ds))
             return rc;
         if (int rc = process_input(ds, device_frame))
@@ -1194,36 +1362,7 @@ aqz_ds_take_frame(aqz_ds* ds,
         *has_frame = 0;
         if (int rc = settle(ds))
             return rc;
-        if (level == 0 || level >= ds->n)
-            return AQZ_OK; // the reference's map lookup simply misses
-        if (ds->cached[level] < 0)
-            return AQZ_OK;
-        *has_frame = 1;
-        if (nbytes)
-            *nbytes = ds->bytes[level];
-        if (!dst)
-            return AQZ_OK;
-        if (cap < ds->bytes[level])
-            return ds->fail_arg("take_frame: buffer too small");
-        if (int rc = bind_device(ds))
-            return rc;
-        if (ds->eager && ds->host_for[level] == ds->cached[level]) {
-            // already on its way to pinned memory (eager_readback)
-            HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
-            std::memcpy(dst, ds->h_level[level], ds->bytes[level]);
-        } else {
-            // HBM -> caller memory directly (stream-ordered after the kernels)
-            HIP_TRY(ds,
-                    hipMemcpyAsync(dst, ds->slot_ptr(level, ds->cached[level]),
-                                   ds->bytes[level], hipMemcpyDeviceToHost, ds->stream),
-                    "hipMemcpyAsync D2H");
-            HIP_TRY(ds, hipStreamSynchronize(ds->stream), "hipStreamSynchronize");
-        }
-        ds->cached[level] = -1;
-        ds->tiled_for[level] = -1;
-        ds->host_for[level] = -1;
-        ds->htile_for[level] = -1;
-        return AQZ_OK;
+        return take_plain(ds, level, dst, cap, nbytes, has_frame);
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
     }
@@ -1299,48 +1438,8 @@ aqz_ds_take_frame_tiled(aqz_ds* ds,
         *has_frame = 0;
         if (int rc = settle(ds))
             return rc;
-        if (tile_rows == 0 || tile_cols == 0)
-            return ds->fail_arg("take_frame_tiled: empty tile");
-        if (level == 0 || level >= ds->n || ds->cached[level] < 0)
-            return AQZ_OK;
-        const TileGeom g = tile_geom(ds, level, tile_rows, tile_cols);
-        *has_frame = 1;
-        if (nbytes)
-            *nbytes = g.tile_bytes;
-        if (!dst)
-            return AQZ_OK;
-        if (cap < g.tile_bytes)
-            return ds->fail_arg("take_frame_tiled: buffer too small");
-        if (int rc = bind_device(ds))
-            return rc;
-        const int k = ds->cached[level];
-        if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
-            ds->tiled_for[level] == k && ds->htile_for[level] == k) {
-            // tiled and copied out when the frame was emitted (eager readback)
-            HIP_TRY(ds, hipEventSynchronize(ds->levels_d2h), "hipEventSynchronize");
-            std::memcpy(dst, ds->h_tiles[level], g.tile_bytes);
-            if (tile_nonzero)
-                reduce_slice_flags(g, ds->tflag_slices[level][k],
-                                   k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
-                                   tile_nonzero);
-        } else if (ds->tiling[level] == std::make_pair(tile_rows, tile_cols) &&
-                   ds->tiled_for[level] == k) {
-            // tiled when the frame was emitted (aqz_ds_set_level_tiling)
-            if (int rc = tiles_to_host(ds, g, ds->tflag_slices[level][k],
-                                       k == 0 ? ds->tslot[level].first : ds->tslot[level].second,
-                                       k == 0 ? ds->tflags[level].first : ds->tflags[level].second,
-                                       dst, tile_nonzero))
-                return rc;
-        } else if (int rc = tile_to_host(ds, ds->slot_ptr(level, k), ds->lv[level], tile_rows,
-                                         tile_cols, g, dst, tile_nonzero)) {
-            return rc;
-        }
-        ds->cached[level] = -1;
-        ds->tiled_for[level] = -1;
-        ds->host_for[level] = -1;
-        ds->htile_for[level] = -1;
-        ds->no_eager[level] = 1; // this caller takes the level tiled
-        return AQZ_OK;
+        return take_tiled(ds, level, tile_rows, tile_cols, dst, cap, tile_nonzero, nbytes,
+                          has_frame);
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
     }

@@ -985,6 +985,7 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
         res["tiled_one_pass_runs"] = ds.stream_tiled_runs()
         res["async_overlap"] = measure_async_overlap(ds, geo, frames, n_frames, tile)
         res["async_overlap_ms_per_frame"] = res["async_overlap"]["async_overlap_ms_per_frame"]
+        res["async_take_ms_per_frame"] = res["async_overlap"]["async_take_ms_per_frame"]
     ds.close()
     return res
 
@@ -1048,6 +1049,19 @@ def measure_async_overlap(ds, geo, frames, n_frames, tile):
         ds.wait()
         last_async = takes()
     overlap = (time.perf_counter() - t0) / n_frames
+    # the takes in the background job too (aqz_ds_add_frame_async_take):
+    # the levels' D2H overlaps the host tiling as the upload does
+    tl = [None] + [tuple(tile)] * (n_lv - 1)
+    for i in range(3):
+        ds.add_frame_async_take(frames[i % 4], tl)
+        tiler(frames[i % 4])
+        ds.wait_takes()
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        ds.add_frame_async_take(frames[i % 4], tl)
+        tiler(frames[i % 4])
+        last_take = ds.wait_takes()[1:]
+    overlap_take = (time.perf_counter() - t0) / n_frames
     t0 = time.perf_counter()
     for i in range(n_frames):
         ds.add_frame(frames[i % 4])
@@ -1060,9 +1074,12 @@ def measure_async_overlap(ds, geo, frames, n_frames, tile):
     host = (time.perf_counter() - t0) / n_frames
     tiler.close()
     # both loops end on frames[(n_frames - 1) % 4]
-    same = all(a is not None and b is not None and np.array_equal(a[0], b[0]) and
-               np.array_equal(a[1], b[1]) for a, b in zip(last_async, last_sync))
+    same = all(a is not None and b is not None and c is not None and
+               np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and
+               np.array_equal(c[0].reshape(-1), b[0].reshape(-1)) and np.array_equal(c[1], b[1])
+               for a, b, c in zip(last_async, last_sync, last_take))
     return {"async_overlap_ms_per_frame": round(overlap * 1e3, 3),
+            "async_take_ms_per_frame": round(overlap_take * 1e3, 3),
             "sequential_ms_per_frame": round(seq * 1e3, 3),
             "host_l0_tiling_ms_per_frame": round(host * 1e3, 3),
             "host_threads": 16,

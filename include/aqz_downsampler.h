@@ -185,6 +185,48 @@ int aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes);
 int aqz_ds_wait(aqz_ds* ds);
 
 /*
+ * One level's part in aqz_ds_add_frame_async_take.
+ *   mode AQZ_TAKE_NONE: nothing (the level is taken later, or not at all);
+ *   AQZ_TAKE_INTO: right behind the add, take the level's frame if it has
+ *     one — chunk-tiled into `dst` like aqz_ds_take_frame_tiled when
+ *     tile_rows/tile_cols are nonzero (`tile_nonzero` optional), row-major
+ *     like aqz_ds_take_frame when both are 0 — and report has_frame/nbytes;
+ *   AQZ_TAKE_HOLD: the caller still holds an untaken frame of this level
+ *     from an earlier INTO take, so this add's frame at the level is dropped,
+ *     as Downsampler::emplace_downsampled_frame_ drops a frame while one is
+ *     cached (downsampler.cpp:599-605).
+ */
+#define AQZ_TAKE_NONE 0
+#define AQZ_TAKE_INTO 1
+#define AQZ_TAKE_HOLD 2
+typedef struct
+{
+    int mode;
+    uint32_t tile_rows, tile_cols;
+    void* dst;
+    size_t cap;
+    uint8_t* tile_nonzero;
+    size_t nbytes;  /* out */
+    int has_frame;  /* out */
+} aqz_level_take;
+
+/*
+ * aqz_ds_add_frame_async plus, in the same background job, the takes
+ * MultiscaleArray::write_multiscale_frames_ makes right after add_frame
+ * (multiscale.array.cpp:298-325): `takes[L]` for every level L >= 1 (index 0
+ * ignored).  The levels' device-to-host copies then overlap the caller's own
+ * work as the upload does.  `host_frame`, `takes` and every buffer they name
+ * must stay valid until aqz_ds_wait returns; the outputs are valid once it
+ * has returned AQZ_OK.  Same results as aqz_ds_add_frame followed by the
+ * takes.  aqz_ds_add_frame, _add_frame_async and _add_device_frame end any
+ * hold.
+ */
+int aqz_ds_add_frame_async_take(aqz_ds* ds,
+                                const void* host_frame,
+                                size_t nbytes,
+                                aqz_level_take* takes);
+
+/*
  * Transposed storage order (`transpose_frame`,
  * array.cpp:488-504).  When the array's storage_dimension_order swaps Y and X
  * (`ArrayDimensions::needs_xy_transposition`, array.dimensions.cpp:563-576),

@@ -9,7 +9,7 @@
 //   ~Downsampler()               (implicit)               -> aqz_ds_destroy
 //   add_frame(frame)             downsampler.cpp:306-401  -> aqz_ds_add_frame
 //   take_frame(level, out)       downsampler.cpp:403-414  -> aqz_ds_take_frame
-//   add_frame_async(frame)       new -> aqz_ds_add_frame_async
+//   add_frame_async(frame)       new -> aqz_ds_add_frame_async_take
 //   wait()                       new                      -> aqz_ds_wait
 //   take_frame_tiled(level, t)   new -> aqz_ds_take_frame_tiled
 //   level_is_tiled(level)        new
@@ -89,6 +89,9 @@ zarr::Downsampler::Downsampler(std::shared_ptr<ArrayConfig> config,
     // (array.tiled.cpp).  A transposed storage order keeps the row-major
     // path: Array chunks the transpose of what it is given.
     tiles_.assign(n, { 0u, 0u });
+    takes_.assign(n, aqz_level_take{});
+    taken_.assign(n, {});
+    holding_.assign(n, 0);
     if (config->dimensions->needs_xy_transposition()) {
         return;
     }
@@ -115,6 +118,15 @@ zarr::Downsampler::~Downsampler()
 void
 zarr::Downsampler::add_frame(std::vector<uint8_t>& frame)
 {
+    for (const uint8_t h : holding_) {
+        if (h) {
+            // frames taken ahead are still unconsumed: their levels must drop
+            // this frame's results, as a cached frame would
+            add_frame_async(frame);
+            wait();
+            return;
+        }
+    }
     const int rc = aqz_ds_add_frame(gpu_, frame.data(), frame.size());
     EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
 }
@@ -122,15 +134,70 @@ zarr::Downsampler::add_frame(std::vector<uint8_t>& frame)
 void
 zarr::Downsampler::add_frame_async(std::vector<uint8_t>& frame)
 {
-    const int rc = aqz_ds_add_frame_async(gpu_, frame.data(), frame.size());
+    // The takes write_multiscale_frames_ makes right after the add
+    // (multiscale.array.cpp:298-325) run in the same background job, so the
+    // levels' device-to-host copies overlap level 0's chunking too.  A level
+    // whose earlier frame is still unconsumed here is held instead.
+    for (size_t level = 1; level < takes_.size(); ++level) {
+        aqz_level_take& t = takes_[level];
+        t = aqz_level_take{};
+        if (holding_[level]) {
+            t.mode = AQZ_TAKE_HOLD;
+            continue;
+        }
+        const auto [tile_rows, tile_cols] = tiles_[level];
+        size_t bytes = aqz_ds_level_bytes(gpu_, uint32_t(level));
+        if (tile_rows != 0) {
+            const auto& dims = writer_configurations_.at(int(level))->dimensions;
+            const size_t w = dims->width_dim().array_size_px;
+            const size_t h = dims->height_dim().array_size_px;
+            bytes = ((w + tile_cols - 1) / tile_cols) * ((h + tile_rows - 1) / tile_rows) *
+                    tile_rows * tile_cols * (bytes / (w * h));
+        }
+        // a vector the caller swapped back keeps its capacity: no new
+        // allocation once both have reached the level's size
+        taken_[level].resize(bytes);
+        t.mode = AQZ_TAKE_INTO;
+        t.tile_rows = tile_rows;
+        t.tile_cols = tile_cols;
+        t.dst = taken_[level].data();
+        t.cap = taken_[level].size();
+    }
+    const int rc =
+      aqz_ds_add_frame_async_take(gpu_, frame.data(), frame.size(), takes_.data());
     EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+    pending_ = true;
 }
 
 void
 zarr::Downsampler::wait()
 {
     const int rc = aqz_ds_wait(gpu_);
+    const bool had_takes = pending_;
+    pending_ = false;
     EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_ds_last_error(gpu_));
+    if (!had_takes) {
+        return;
+    }
+    for (size_t level = 1; level < takes_.size(); ++level) {
+        if (takes_[level].mode == AQZ_TAKE_INTO && takes_[level].has_frame) {
+            holding_[level] = 1;
+        }
+    }
+}
+
+bool
+zarr::Downsampler::hand_over_(int level, std::vector<uint8_t>& out)
+{
+    if (level < 1 || static_cast<size_t>(level) >= holding_.size() || !holding_[level]) {
+        return false;
+    }
+    if (pending_) {
+        wait();
+    }
+    out.swap(taken_[level]); // handed over by swap, as downsampler.cpp:403-414
+    holding_[level] = 0;
+    return true;
 }
 
 bool
@@ -140,6 +207,12 @@ zarr::Downsampler::take_frame(int level, std::vector<uint8_t>& frame_data)
     // including out-of-range ones (downsampler.cpp:403-414).
     if (level < 1 || static_cast<size_t>(level) >= n_levels_()) {
         return false;
+    }
+    if (pending_) {
+        wait();
+    }
+    if (!level_is_tiled(level) && hand_over_(level, frame_data)) {
+        return true; // taken in the add's background job
     }
     // Size query first: the frame stays cached until it is copied out.
     size_t nbytes = 0;
@@ -175,6 +248,12 @@ zarr::Downsampler::take_frame_tiled(int level, std::vector<uint8_t>& tiles)
 {
     if (!level_is_tiled(level)) {
         return false;
+    }
+    if (pending_) {
+        wait();
+    }
+    if (hand_over_(level, tiles)) {
+        return true; // taken, tiled, in the add's background job
     }
     const auto [tile_rows, tile_cols] = tiles_[level];
     size_t nbytes = 0;

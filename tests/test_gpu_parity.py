@@ -681,6 +681,62 @@ def test_add_frame_async_tiled_takes(aqz, oracle, shape, tile):
     ds.close()
 
 
+@pytest.mark.parametrize("geo_kind", ["2d_tiled", "2d_plain", "3d_plain", "3d_tiled"])
+def test_add_frame_async_take(aqz, oracle, geo_kind):
+    """aqz_ds_add_frame_async_take: every level taken in the background job
+    right behind the add, equal to add_frame + take_frame(_tiled) of the
+    oracle frame by frame, readiness included.  Frame 1's level 2 is kept by
+    the caller unconsumed across frame 2, whose add holds level 2
+    (AQZ_TAKE_HOLD): frame 2's level-2 frame must be dropped, as the
+    reference's emplace drops a frame while one is cached."""
+    if geo_kind.startswith("2d"):
+        geo = halving_geometry(1000, 601, 4)
+        shape = (601, 1000)
+    else:
+        geo = [(256, 128, 9), (128, 64, 5), (64, 32, 3), (32, 16, 2)]
+        shape = (128, 256)
+    tiled = geo_kind.endswith("tiled")
+    tile = (16, 32)
+    tiles = [None] + [tile] * (len(geo) - 1) if tiled else None
+    ds = aqz.Downsampler(geo, np.uint16, 1)
+    if tiled:
+        for L in range(1, len(geo)):
+            ds.set_level_tiling(L, *tile)
+    ref = oracle.OracleDownsampler(geo, np.uint16, 1)
+    rng = np.random.default_rng(seed_of("async_take", geo_kind))
+
+    def check(got, want, ctx):
+        assert (got is None) == (want is None), ctx
+        if want is None:
+            return
+        if tiled:
+            t, nz = oracle.tile_frame(want, *tile)
+            assert_parity(got[0], t, ctx)
+            assert np.array_equal(got[1], nz), ctx
+        else:
+            assert_parity(got, want, ctx)
+
+    kept = None
+    for i in range(7):
+        f = rng.integers(0, 65536, shape, dtype=np.uint16)
+        f[: shape[0] // 3, : shape[1] // 3] = 0
+        hold = (2,) if (i == 2 and kept is not None) else ()
+        ds.add_frame_async_take(f, tiles, hold)
+        ref.add_frame(f)
+        res = ds.wait_takes()
+        for L in range(1, len(geo)):
+            if L in hold:
+                assert res[L] is None
+                continue
+            if i == 1 and L == 2 and res[L] is not None:
+                kept = res[L]  # the caller keeps it unconsumed for a frame
+                continue
+            check(res[L], ref.take_frame(L), f"frame {i} L{L}")
+        if i == 2 and kept is not None:
+            check(kept, ref.take_frame(2), "held level-2 frame")
+    ds.close()
+
+
 def test_add_frame_async_temporaries(aqz, oracle):
     """Frames passed as temporaries: the binding must keep each one alive
     until the next call has settled its upload.  Each temporary

@@ -137,7 +137,7 @@ def test_adapter_links_against_the_c_abi(tree, tmp_path):
                           "zarr::chunks_along_dimension(ZarrDimension const&)",
                           "zarr::shards_along_dimension(ZarrDimension const&)"}, unresolved
     nm = "\n".join(undef)
-    for sym in ("aqz_ds_create", "aqz_ds_add_frame", "aqz_ds_add_frame_async",
+    for sym in ("aqz_ds_create", "aqz_ds_add_frame", "aqz_ds_add_frame_async_take",
                 "aqz_ds_wait", "aqz_ds_take_frame", "aqz_ds_take_frame_tiled",
                 "aqz_ds_set_level_tiling", "aqz_ds_destroy"):
         assert sym in nm, sym
