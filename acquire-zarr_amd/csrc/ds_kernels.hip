@@ -1938,11 +1938,15 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
             stage_mask = all_levels;
             wide_max = 8;
-            // $AQZ_BAND_SEG4=1 (A/B): 4-tile segments, so that a band whose
-            // LDS leaves room for one workgroup per CU (4096 f32: 85 KiB)
-            // runs two or three, overlapping one's stores with another's loads
-            static const int seg4 = int_env("AQZ_BAND_SEG4", 0);
-            if (seg4 == 1) {
+            // 8-tile bands go in two 4-tile segments: a whole 4096 f32 band
+            // needs 85 KiB of LDS, one workgroup per CU, whose loads and
+            // stores then never overlap; segments fit two or three.  Same
+            // box, two rounds (profiles/r03/f32/band_seg4_ab.log): f32 Max
+            // 1062 -> 999 us, Mean 1042 -> 991, Min 1064 -> 998, the headline
+            // 478 -> 473; 6-tile bands lost (3072^2 470 -> 510), so only
+            // bands of 8.  $AQZ_BAND_SEG4=0 / 1: never / always.
+            static const int seg4 = int_env("AQZ_BAND_SEG4", -1);
+            if (seg4 == 1 || (seg4 < 0 && band_waves == 8)) {
                 seg_tiles = 4;
                 band_waves = 4;
             }
