@@ -373,6 +373,8 @@ struct CascadeParams
     uint32_t order;                  // unit order: 0 columns fastest, 1 frames, 2 row bands
     uint32_t seg_w;                  // > 0: a workgroup is seg_w column tiles of one row band
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
+    uint32_t band_last;              // K > 0: the band's last K waves to finish store it (no barrier)
+    uint32_t band_edges;             // 1: edge mode for whole misaligned bands (StageCtx::edges)
 };
 
 // $AQZ_LOAD_NT: 1 / 0 forces the fused cascade's loads with / without the
@@ -809,7 +811,75 @@ struct StageCtx
     // level width and 0 for a whole band, the segment's for a segmented one
     uint32_t stride[kMaxFusedLevels];
     uint32_t scol[kMaxFusedLevels];
+    // Edge mode (whole misaligned bands, CascadeParams::band_edges): each
+    // wave stores the 64-B bursts that lie wholly in its own tile's columns
+    // straight from registers and stages only the rest, the bursts it
+    // shares with a neighbouring tile (or the row before or after), for the
+    // band's last wave to store whole (band_store_shared_bursts).
+    uint32_t edges;
+    uint32_t tile;                   // the wave's tile in the band
+    uint8_t* gspan[kMaxFusedLevels]; // span byte 0 in global memory
+    uint32_t wb[kMaxFusedLevels];    // level row bytes
+    uint32_t twb[kMaxFusedLevels];   // a tile's columns at the level, bytes
 };
+
+// Edge mode: this wave's block of level J goes to global memory where its
+// bytes fall in a burst wholly inside the wave's tile columns of that row,
+// and to the band's LDS image otherwise (see StageCtx::edges).
+template<typename T, int C, int J, int RO, int CO, bool EDGE>
+__device__ __forceinline__ void
+edge_stage_level(const StageCtx& sc,
+                 const T (&out)[RO][CO],
+                 uint32_t wout,
+                 uint32_t hout,
+                 uint32_t col0,
+                 uint32_t row0,
+                 uint32_t band_row0,
+                 int lane)
+{
+    constexpr int SO = kLaneStride<C, J>;
+    constexpr uint32_t TB = uint32_t(sizeof(T));
+    constexpr int I = J - 1;
+    const uint32_t cout0 = col0 >> J;
+    const uint32_t rout0 = row0 >> J;
+    const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
+    uint8_t* lspan = sc.lds[I] + sc.head[I]; // span byte 0 in LDS
+    uint8_t* g = sc.gspan[I];
+    const int64_t gs = int64_t(reinterpret_cast<uintptr_t>(g));
+    const uint32_t wb = sc.wb[I];
+    const uint32_t t0 = sc.tile * sc.twb[I];
+    const uint32_t t1 = min(t0 + sc.twb[I], wb);
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+        bool ok = leader;
+        if constexpr (EDGE) {
+            ok = ok && (rout0 + r < hout) && (cout0 < wout);
+        }
+        if (!ok)
+            continue;
+        const uint32_t rb = (rout0 + r - (band_row0 >> J)) * wb; // row's first span byte
+        // [lo, hi): span bytes of the bursts wholly inside this wave's columns
+        const int64_t lo = ((gs + rb + t0 + 63) & ~int64_t(63)) - gs;
+        const int64_t hi = ((gs + rb + t1) & ~int64_t(63)) - gs;
+        const uint32_t o = rb + cout0 * TB;
+        if ((!EDGE || cout0 + CO <= wout) && int64_t(o) >= lo && int64_t(o + CO * TB) <= hi) {
+            store_vec<T, CO, true>(reinterpret_cast<T*>(g + o), out[r]);
+            continue;
+        }
+#pragma unroll
+        for (int c = 0; c < CO; ++c) {
+            if (EDGE && cout0 + c >= wout)
+                continue;
+            const uint32_t oc = o + uint32_t(c) * TB;
+            if (int64_t(oc) >= lo && int64_t(oc + TB) <= hi) {
+                const T one[1] = { out[r][c] };
+                store_vec<T, 1, true>(reinterpret_cast<T*>(g + oc), one);
+            } else {
+                *reinterpret_cast<T*>(lspan + oc) = out[r][c];
+            }
+        }
+    }
+}
 
 template<typename T, int C, int J, int RO, int CO, bool EDGE>
 __device__ __forceinline__ void
@@ -902,8 +972,12 @@ cascade_level(const CascadeParams& p,
     } else if constexpr (STAGED) {
         if ((sc->mask >> (J - 1)) & 1u) {
             // the band's rows start at row0 - row0 % 2^NL: one band per block
-            stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
-                                               row0 & ~((1u << NL) - 1u), lane);
+            if (sc->edges)
+                edge_stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0,
+                                                        row0, row0 & ~((1u << NL) - 1u), lane);
+            else
+                stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
+                                                   row0 & ~((1u << NL) - 1u), lane);
         } else {
             store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
                                                     col0, row0, lane);
@@ -1105,6 +1179,25 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         }
         sc.lds[i] = band_lds + off;
         off += (sc.head[i] + len[i] + 15u) & ~15u;
+        sc.gspan[i] = span[i];
+        sc.wb[i] = p.w[i] * uint32_t(sizeof(T));
+        sc.twb[i] = ((64u * C) >> (i + 1)) * uint32_t(sizeof(T));
+    }
+    // edge mode: whole bands only, with the last wave storing (see StageCtx)
+    const bool edges = p.band_edges != 0 && seg_tiles == 0;
+    sc.edges = edges ? 1u : 0u;
+    sc.tile = ux;
+
+    // p.band_last: no barrier before the stores.  Each wave counts itself
+    // in once its LDS writes are done, and the last one to arrive stores the
+    // whole band, so no wave waits for a slower one (the band's partial edge
+    // tile; profiles/r02/band8/misaligned_pmc/).
+    __shared__ uint32_t band_arrivals;
+    const bool last_mode = p.band_last != 0; // uniform
+    if (last_mode) {
+        if (threadIdx.x == 0)
+            band_arrivals = 0;
+        __syncthreads();
     }
 
     if (ux < p.units_x) { // wave-uniform
@@ -1115,7 +1208,78 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         else
             cascade_unit<T, M, NL, C, NT, true, true, true>(p, f, row0, col0, lane, &sc);
     }
-    __syncthreads();
+    uint32_t tid = threadIdx.x, nth = blockDim.x;
+    if (last_mode) {
+        // release: this wave's LDS writes complete before its count lands;
+        // acquire: the storing waves then see every other wave's.  The last
+        // K = p.band_last waves to arrive store the band together; all but
+        // the very last wait for the stragglers among them (the workgroup's
+        // waves are co-resident, so the count always completes).
+        const uint32_t nw = blockDim.x >> 6;
+        const uint32_t K = min(p.band_last, nw);
+        uint32_t old = 0;
+        if (lane == 0)
+            old = __hip_atomic_fetch_add(&band_arrivals, 1u, __ATOMIC_ACQ_REL,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (old + K < nw)
+            return;
+        if (old + 1u < nw) {
+            while (__hip_atomic_load(&band_arrivals, __ATOMIC_ACQUIRE,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP) < nw)
+                __builtin_amdgcn_s_sleep(1);
+        }
+        tid = (old + K - nw) * 64u + uint32_t(lane);
+        nth = K * 64u;
+    } else {
+        __syncthreads();
+    }
+
+    if (edges) {
+        // Edge mode: the bursts that straddle a tile boundary (a row's tile
+        // starts, the span's end) are complete in LDS now; store each whole.
+        // Every other burst of the span went out from its wave's registers.
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            if (!((stage_mask >> i) & 1u) || len[i] == 0)
+                continue;
+            const uint32_t wb = sc.wb[i], twb = sc.twb[i], n = p.units_x;
+            const uint32_t L = len[i];
+            const uint32_t nb = rows_of[i] * n + 1u; // tile starts, then the span's end
+            uint8_t* g = span[i];
+            const uintptr_t gs = reinterpret_cast<uintptr_t>(g);
+            uint8_t* lspan = sc.lds[i] + sc.head[i];
+            for (uint32_t k = tid; k < nb * 4u; k += nth) {
+                const uint32_t q = k >> 2, part = k & 3u;
+                uint32_t b;
+                if (q + 1u < nb) {
+                    const uint32_t rr = q / n, t = q - rr * n;
+                    if (t * twb >= wb)
+                        continue;
+                    b = rr * wb + t * twb;
+                } else {
+                    b = L;
+                }
+                const uintptr_t at = gs + b;
+                if ((at & 63u) == 0)
+                    continue; // a burst edge: nothing shared there
+                // 16-B chunk `part` of the burst holding byte b, clipped to the span
+                const int64_t c0 = int64_t((at & ~uintptr_t(63)) + part * 16u) - int64_t(gs);
+                const int64_t lo = c0 > 0 ? c0 : 0;
+                const int64_t hi = c0 + 16 < int64_t(L) ? c0 + 16 : int64_t(L);
+                if (lo >= hi)
+                    continue;
+                if (lo == c0 && hi == c0 + 16) {
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(lspan + c0);
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(g + c0));
+                } else {
+                    for (int64_t x = lo; x < hi; ++x)
+                        g[x] = lspan[x];
+                }
+            }
+        }
+        return;
+    }
 
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
@@ -1126,7 +1290,7 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
             const uint32_t cpr = piece[i] / 16u;
             const uint32_t chunks = rows_of[i] * cpr;
             const uint64_t pitch = uint64_t(p.w[i]) * sizeof(T);
-            for (uint32_t k = threadIdx.x; k < chunks; k += blockDim.x) {
+            for (uint32_t k = tid; k < chunks; k += nth) {
                 const uint32_t r = k / cpr, c = k - r * cpr;
                 const u32x4 v = *reinterpret_cast<const u32x4*>(sc.lds[i] + r * piece[i] + c * 16u);
                 __builtin_nontemporal_store(
@@ -1138,7 +1302,7 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         const uint32_t end = head + len[i];
         const uint32_t chunks = (end + 15u) / 16u;
         uint8_t* g = span[i] - head;
-        for (uint32_t k = threadIdx.x; k < chunks; k += blockDim.x) {
+        for (uint32_t k = tid; k < chunks; k += nth) {
             const uint32_t a = k * 16u, b = a + 16u;
             if (a >= head && b <= end) {
                 const u32x4 v = *reinterpret_cast<const u32x4*>(sc.lds[i] + a);
@@ -1164,8 +1328,8 @@ band_lds_cap()
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) ==
               hipSuccess &&
-            v > 0)
-            c = uint32_t(v);
+            v > 16)
+            c = uint32_t(v) - 16u; // the kernel's static arrival counter
         const int e = int_env("AQZ_BAND_LDS_CAP", 0);
         return e > 0 ? std::min(c, uint32_t(e)) : c;
     }();
@@ -1893,11 +2057,21 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         p.wb = store_wb_env() >= 0 ? uint32_t(store_wb_env()) : 0u;
         p.nt = load_nt(W, sizeof(T));
         // Band staging when some level's rows are not whole 64-byte bursts
-        // and a row band is at most 4 tiles ($AQZ_BAND_STAGING=0: never).
-        // Wider bands would need bigger workgroups, and a workgroup that
-        // waits for its slowest wave before storing costs more than it saves:
-        // 8- and 16-wave bands measured 30% and 50% slower than 4-wave ones
-        // (profiles/r01/shape_sweep_band.log).
+        // and a row band is at most 6 tiles ($AQZ_BAND_STAGING=0: never;
+        // $AQZ_BAND_MIS_MAX: the widest such band, default 6).  These bands
+        // are stored by their last wave to finish (p.band_last = 1), not
+        // after a barrier: any wait for the band's slowest wave cost more
+        // than staging saves (3000^2 805 us with a barrier, 594 / 676 us with
+        // the last two / three waves storing, 546 us with the last one,
+        // against 575 us for direct stores; 2000^2 549 -> 524 us against the
+        // barrier; profiles/r03/misaligned/last_wave_ab.log).  Above 6 tiles
+        // one wave storing the band is too slow (4000x3000 557 -> 627 us),
+        // so wider misaligned bands keep direct stores.  Aligned bands keep
+        // the barrier, where all waves share the stores (4096^2 f32 987 us
+        // against 1026 / 1058 us).  $AQZ_BAND_LAST=K forces the last K waves
+        // to store every band (0: the barrier).
+        static const int band_last_env = int_env("AQZ_BAND_LAST", -1);
+        static const uint32_t mis_max = uint32_t(std::clamp(int_env("AQZ_BAND_MIS_MAX", 6), 0, 8));
         uint32_t stage_mask = 0;
         for (int i = 0; i < n_out; ++i) {
             const bool whole = (uint64_t(outs[i].w) * sizeof(T)) % 64 == 0 &&
@@ -1916,8 +2090,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // On most MI355X boxes tried, row-major level rows at a >= 4 KiB
         // pitch written 512 B per wave ran 15-20% below the same kernel with
         // tile-order stores; staged bands remove that (headline 535 -> 463
-        // us, 3072^2 541 -> 448 us; profiles/r02/band8_*).  Misaligned
-        // bands that wide stay direct: staging them cost 27% at 3000^2.
+        // us, 3072^2 541 -> 448 us; profiles/r02/band8_*).
         // $AQZ_BAND_ALIGNED=0 turns this off; $AQZ_BAND_FORCE (A/B) stages a
         // level mask whatever the alignment, in bands of up to 8 waves.
         // Aligned bands wider than 8 tiles go in 8-tile segments, one
@@ -1930,7 +2103,12 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         static const bool band_segments = int_env("AQZ_BAND_SEGMENTS", 1) != 0;
         uint32_t band_waves = p.units_x;
         const uint32_t all_levels = (1u << n_out) - 1u;
-        uint32_t wide_max = 4, seg_tiles = 0;
+        uint32_t wide_max = mis_max, seg_tiles = 0;
+        const bool misaligned = stage_mask != 0;
+        p.band_last = band_last_env >= 0 ? uint32_t(std::min(band_last_env, 8))
+                                         : (misaligned ? 1u : 0u);
+        static const int band_edges_env = int_env("AQZ_BAND_EDGES", 0);
+        p.band_edges = (misaligned && band_edges_env > 0) ? 1u : 0u;
         if (band_force) {
             stage_mask |= band_force & all_levels;
             wide_max = 8;
@@ -1966,7 +2144,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         const uint32_t segs = seg_tiles ? (p.units_x + seg_tiles - 1) / seg_tiles : 1u;
         const uint32_t bands = p.units_y * n_frames * segs;
         // Direct stores of rows that split 64-B bursts, bands wider than the
-        // barrier form takes: one workgroup per band (or per balanced piece
+        // staged form takes: one workgroup per band (or per balanced piece
         // of <= 8 tiles), so a burst shared by neighbouring waves is written
         // through one L2.  3000^2 622 -> 576 us, 2600^2 601 -> 540 us,
         // 5472x3648 571 -> 540 us against 4-wave blocks that straddle bands

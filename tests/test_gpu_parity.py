@@ -180,9 +180,9 @@ BATCH_GEOMETRIES = {
     # units divide by 4: with column edges, and with one fused level (NL = 1)
     "3d_fused_oddw_even_h": ([(201, 64, 8), (101, 32, 4), (51, 16, 2)], 8, 2),
     "3d_fused_one_level": ([(256, 64, 4), (128, 32, 2)], 4, 2),
-    # level rows that split 64-B bursts: band-staged stores (burst
-    # completion) when a row band is <= 8 tiles (u8, u16, f32 here), direct
-    # stores for wider bands (i64)
+    # level rows that split 64-B bursts: band-staged stores when a row band
+    # is <= 4 tiles (1500 px u16), direct stores from band-aligned
+    # workgroups for wider bands (2600 px u16 / f32, i64)
     "2d_wide_misaligned": (halving_geometry(2600, 70, 4), 3, 1),
     "2d_band_staged": (halving_geometry(1500, 90, 4), 3, 1),
     # aligned row bands of 5-8 tiles: every level staged by 8-wave (u16, f32
@@ -192,9 +192,9 @@ BATCH_GEOMETRIES = {
     # aligned bands wider than 8 tiles: 8-tile segments (u8 9 tiles, u16 /
     # f32 17, i64 34), a last segment of one or two tiles, odd band rows
     "2d_band_segments": (halving_geometry(8704, 40, 4), 2, 1),
-    # misaligned bands of up to 8 tiles in burst-completion mode (round 3):
-    # 8 tiles (u16 / f32) with an odd band at the bottom; a last tile of 10
-    # px, so deep levels hold bursts shared by three waves
+    # misaligned bands of up to 8 tiles in band-aligned workgroups (round
+    # 3): 8 tiles (u16 / f32) with an odd band at the bottom; a last tile of
+    # 10 px, so deep levels hold bursts shared by three waves
     "2d_complete_8tile": (halving_geometry(3900, 37, 4), 2, 1),
     "2d_complete_short_last": (halving_geometry(2570, 50, 4), 3, 1),
 }
