@@ -374,7 +374,6 @@ struct CascadeParams
     uint32_t seg_w;                  // > 0: a workgroup is seg_w column tiles of one row band
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
     uint32_t band_last;              // K > 0: the band's last K waves to finish store it (no barrier)
-    uint32_t band_edges;             // 1: edge mode for whole misaligned bands (StageCtx::edges)
 };
 
 // $AQZ_LOAD_NT: 1 / 0 forces the fused cascade's loads with / without the
@@ -811,75 +810,7 @@ struct StageCtx
     // level width and 0 for a whole band, the segment's for a segmented one
     uint32_t stride[kMaxFusedLevels];
     uint32_t scol[kMaxFusedLevels];
-    // Edge mode (whole misaligned bands, CascadeParams::band_edges): each
-    // wave stores the 64-B bursts that lie wholly in its own tile's columns
-    // straight from registers and stages only the rest, the bursts it
-    // shares with a neighbouring tile (or the row before or after), for the
-    // band's last wave to store whole (band_store_shared_bursts).
-    uint32_t edges;
-    uint32_t tile;                   // the wave's tile in the band
-    uint8_t* gspan[kMaxFusedLevels]; // span byte 0 in global memory
-    uint32_t wb[kMaxFusedLevels];    // level row bytes
-    uint32_t twb[kMaxFusedLevels];   // a tile's columns at the level, bytes
 };
-
-// Edge mode: this wave's block of level J goes to global memory where its
-// bytes fall in a burst wholly inside the wave's tile columns of that row,
-// and to the band's LDS image otherwise (see StageCtx::edges).
-template<typename T, int C, int J, int RO, int CO, bool EDGE>
-__device__ __forceinline__ void
-edge_stage_level(const StageCtx& sc,
-                 const T (&out)[RO][CO],
-                 uint32_t wout,
-                 uint32_t hout,
-                 uint32_t col0,
-                 uint32_t row0,
-                 uint32_t band_row0,
-                 int lane)
-{
-    constexpr int SO = kLaneStride<C, J>;
-    constexpr uint32_t TB = uint32_t(sizeof(T));
-    constexpr int I = J - 1;
-    const uint32_t cout0 = col0 >> J;
-    const uint32_t rout0 = row0 >> J;
-    const bool leader = (SO == 1) || ((lane & (SO - 1)) == 0);
-    uint8_t* lspan = sc.lds[I] + sc.head[I]; // span byte 0 in LDS
-    uint8_t* g = sc.gspan[I];
-    const int64_t gs = int64_t(reinterpret_cast<uintptr_t>(g));
-    const uint32_t wb = sc.wb[I];
-    const uint32_t t0 = sc.tile * sc.twb[I];
-    const uint32_t t1 = min(t0 + sc.twb[I], wb);
-#pragma unroll
-    for (int r = 0; r < RO; ++r) {
-        bool ok = leader;
-        if constexpr (EDGE) {
-            ok = ok && (rout0 + r < hout) && (cout0 < wout);
-        }
-        if (!ok)
-            continue;
-        const uint32_t rb = (rout0 + r - (band_row0 >> J)) * wb; // row's first span byte
-        // [lo, hi): span bytes of the bursts wholly inside this wave's columns
-        const int64_t lo = ((gs + rb + t0 + 63) & ~int64_t(63)) - gs;
-        const int64_t hi = ((gs + rb + t1) & ~int64_t(63)) - gs;
-        const uint32_t o = rb + cout0 * TB;
-        if ((!EDGE || cout0 + CO <= wout) && int64_t(o) >= lo && int64_t(o + CO * TB) <= hi) {
-            store_vec<T, CO, true>(reinterpret_cast<T*>(g + o), out[r]);
-            continue;
-        }
-#pragma unroll
-        for (int c = 0; c < CO; ++c) {
-            if (EDGE && cout0 + c >= wout)
-                continue;
-            const uint32_t oc = o + uint32_t(c) * TB;
-            if (int64_t(oc) >= lo && int64_t(oc + TB) <= hi) {
-                const T one[1] = { out[r][c] };
-                store_vec<T, 1, true>(reinterpret_cast<T*>(g + oc), one);
-            } else {
-                *reinterpret_cast<T*>(lspan + oc) = out[r][c];
-            }
-        }
-    }
-}
 
 template<typename T, int C, int J, int RO, int CO, bool EDGE>
 __device__ __forceinline__ void
@@ -972,12 +903,8 @@ cascade_level(const CascadeParams& p,
     } else if constexpr (STAGED) {
         if ((sc->mask >> (J - 1)) & 1u) {
             // the band's rows start at row0 - row0 % 2^NL: one band per block
-            if (sc->edges)
-                edge_stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0,
-                                                        row0, row0 & ~((1u << NL) - 1u), lane);
-            else
-                stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
-                                                   row0 & ~((1u << NL) - 1u), lane);
+            stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
+                                               row0 & ~((1u << NL) - 1u), lane);
         } else {
             store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
                                                     col0, row0, lane);
@@ -1120,10 +1047,12 @@ cascade_kernel(CascadeParams p)
 // adjacent in memory — as one span of whole, 16-byte-aligned chunks, so only
 // the span's first and last chunk share bursts with the neighbouring bands.
 // Used for frames whose level rows split 64-byte bursts (widths like 2000 or
-// 3000 px, bands of <= 4 tiles: partial-burst writes measured 30% slower
-// than whole ones, tools/pitchbench.hip) and for aligned bands of 5-8 tiles
-// (row-major rows at >= 4 KiB pitch written 512 B per wave ran 15% slow on
-// most boxes).  seg_tiles > 0 (aligned frames only): a band wider than that
+// 3000 px, bands of <= 4 tiles, <= 6 for 2-byte types: partial-burst writes
+// measured 30% slower than whole ones, tools/pitchbench.hip), where the
+// band's last wave stores it instead of a barrier (CascadeParams::band_last),
+// and for aligned bands of 5-8 tiles (row-major rows at >= 4 KiB pitch
+// written 512 B per wave ran 15% slow on most boxes).  seg_tiles > 0
+// (aligned frames only): a band wider than that
 // is split into segments of seg_tiles tiles, one workgroup each, every level
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
@@ -1179,14 +1108,7 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         }
         sc.lds[i] = band_lds + off;
         off += (sc.head[i] + len[i] + 15u) & ~15u;
-        sc.gspan[i] = span[i];
-        sc.wb[i] = p.w[i] * uint32_t(sizeof(T));
-        sc.twb[i] = ((64u * C) >> (i + 1)) * uint32_t(sizeof(T));
     }
-    // edge mode: whole bands only, with the last wave storing (see StageCtx)
-    const bool edges = p.band_edges != 0 && seg_tiles == 0;
-    sc.edges = edges ? 1u : 0u;
-    sc.tile = ux;
 
     // p.band_last: no barrier before the stores.  Each wave counts itself
     // in once its LDS writes are done, and the last one to arrive stores the
@@ -1235,51 +1157,6 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         __syncthreads();
     }
 
-    if (edges) {
-        // Edge mode: the bursts that straddle a tile boundary (a row's tile
-        // starts, the span's end) are complete in LDS now; store each whole.
-        // Every other burst of the span went out from its wave's registers.
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            if (!((stage_mask >> i) & 1u) || len[i] == 0)
-                continue;
-            const uint32_t wb = sc.wb[i], twb = sc.twb[i], n = p.units_x;
-            const uint32_t L = len[i];
-            const uint32_t nb = rows_of[i] * n + 1u; // tile starts, then the span's end
-            uint8_t* g = span[i];
-            const uintptr_t gs = reinterpret_cast<uintptr_t>(g);
-            uint8_t* lspan = sc.lds[i] + sc.head[i];
-            for (uint32_t k = tid; k < nb * 4u; k += nth) {
-                const uint32_t q = k >> 2, part = k & 3u;
-                uint32_t b;
-                if (q + 1u < nb) {
-                    const uint32_t rr = q / n, t = q - rr * n;
-                    if (t * twb >= wb)
-                        continue;
-                    b = rr * wb + t * twb;
-                } else {
-                    b = L;
-                }
-                const uintptr_t at = gs + b;
-                if ((at & 63u) == 0)
-                    continue; // a burst edge: nothing shared there
-                // 16-B chunk `part` of the burst holding byte b, clipped to the span
-                const int64_t c0 = int64_t((at & ~uintptr_t(63)) + part * 16u) - int64_t(gs);
-                const int64_t lo = c0 > 0 ? c0 : 0;
-                const int64_t hi = c0 + 16 < int64_t(L) ? c0 + 16 : int64_t(L);
-                if (lo >= hi)
-                    continue;
-                if (lo == c0 && hi == c0 + 16) {
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(lspan + c0);
-                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(g + c0));
-                } else {
-                    for (int64_t x = lo; x < hi; ++x)
-                        g[x] = lspan[x];
-                }
-            }
-        }
-        return;
-    }
 
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
@@ -2057,21 +1934,29 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         p.wb = store_wb_env() >= 0 ? uint32_t(store_wb_env()) : 0u;
         p.nt = load_nt(W, sizeof(T));
         // Band staging when some level's rows are not whole 64-byte bursts
-        // and a row band is at most 6 tiles ($AQZ_BAND_STAGING=0: never;
-        // $AQZ_BAND_MIS_MAX: the widest such band, default 6).  These bands
-        // are stored by their last wave to finish (p.band_last = 1), not
-        // after a barrier: any wait for the band's slowest wave cost more
-        // than staging saves (3000^2 805 us with a barrier, 594 / 676 us with
-        // the last two / three waves storing, 546 us with the last one,
-        // against 575 us for direct stores; 2000^2 549 -> 524 us against the
-        // barrier; profiles/r03/misaligned/last_wave_ab.log).  Above 6 tiles
-        // one wave storing the band is too slow (4000x3000 557 -> 627 us),
-        // so wider misaligned bands keep direct stores.  Aligned bands keep
-        // the barrier, where all waves share the stores (4096^2 f32 987 us
-        // against 1026 / 1058 us).  $AQZ_BAND_LAST=K forces the last K waves
-        // to store every band (0: the barrier).
+        // and a row band is at most 4 tiles, 6 for 2-byte types
+        // ($AQZ_BAND_STAGING=0: never; $AQZ_BAND_MIS_MAX: the widest such
+        // band).  These bands are stored by their last wave to finish
+        // (p.band_last = 1), not after a barrier: any wait for the band's
+        // slowest wave cost more than staging saves (u16 3000^2 805 us with
+        // a barrier, 594 / 676 us with the last two / three waves storing,
+        // 546 us with the last one, against 575 us for direct stores;
+        // profiles/r03/misaligned/last_wave_ab.log).  Against the barrier
+        // form of <= 4 tiles and direct stores above (mis6_edges_ab.log):
+        // u16 2000^2 570 -> 523 us, 2304^2 565 -> 498, 3000^2 575 -> 549,
+        // 2600^2 538 -> 547; u8 3000^2 104 -> 85; f32 2000^2 unchanged.
+        // One wave storing a wider band is too slow: u16 4000x3000 (8 tiles)
+        // 557 -> 627 us, u8 5000x4000 (5 tiles) 91 -> 101, f32 3000^2 (6
+        // tiles, 64 KiB) 1095 -> 1442, so those keep direct stores.  Aligned
+        // bands keep the barrier, where all waves share the stores (4096^2
+        // f32 987 us against 1026 / 1058 us).  $AQZ_BAND_LAST=K forces the
+        // last K waves to store every band (0: the barrier).  Also tried and
+        // dropped: waves storing the bursts inside their own tile from
+        // registers and the last wave only the shared ones (5-27% slower).
         static const int band_last_env = int_env("AQZ_BAND_LAST", -1);
-        static const uint32_t mis_max = uint32_t(std::clamp(int_env("AQZ_BAND_MIS_MAX", 6), 0, 8));
+        static const int mis_max_env = int_env("AQZ_BAND_MIS_MAX", -1);
+        const uint32_t mis_max = mis_max_env >= 0 ? uint32_t(std::min(mis_max_env, 8))
+                                                  : (sizeof(T) == 2 ? 6u : 4u);
         uint32_t stage_mask = 0;
         for (int i = 0; i < n_out; ++i) {
             const bool whole = (uint64_t(outs[i].w) * sizeof(T)) % 64 == 0 &&
@@ -2107,8 +1992,6 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         const bool misaligned = stage_mask != 0;
         p.band_last = band_last_env >= 0 ? uint32_t(std::min(band_last_env, 8))
                                          : (misaligned ? 1u : 0u);
-        static const int band_edges_env = int_env("AQZ_BAND_EDGES", 0);
-        p.band_edges = (misaligned && band_edges_env > 0) ? 1u : 0u;
         if (band_force) {
             stage_mask |= band_force & all_levels;
             wide_max = 8;
