@@ -374,6 +374,7 @@ struct CascadeParams
     uint32_t seg_w;                  // > 0: a workgroup is seg_w column tiles of one row band
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
     uint32_t band_last;              // K > 0: the band's last K waves to finish store it (no barrier)
+    uint32_t seg_rowwise;            // 1: band segments of misaligned rows (StageCtx::rowb)
 };
 
 // $AQZ_LOAD_NT: 1 / 0 forces the fused cascade's loads with / without the
@@ -810,6 +811,12 @@ struct StageCtx
     // level width and 0 for a whole band, the segment's for a segmented one
     uint32_t stride[kMaxFusedLevels];
     uint32_t scol[kMaxFusedLevels];
+    // Misaligned segments (rowb > 0): each level row of the segment is its
+    // own piece in LDS, rowb bytes apart, placed at the same offset modulo
+    // 16 as its global address, so that it leaves in aligned 16-byte chunks:
+    // row r's piece starts (head + r * hstep) % 16 bytes into its slot.
+    uint32_t rowb[kMaxFusedLevels];
+    uint32_t hstep[kMaxFusedLevels];
 };
 
 template<typename T, int C, int J, int RO, int CO, bool EDGE>
@@ -836,8 +843,16 @@ stage_level(const StageCtx& sc,
         }
         if (!ok)
             continue;
-        T* d = reinterpret_cast<T*>(base) +
-               uint64_t(rout0 + r - (band_row0 >> J)) * sc.stride[J - 1] + (cout0 - sc.scol[J - 1]);
+        const uint32_t rr = rout0 + r - (band_row0 >> J); // row within the band
+        T* d;
+        if (sc.rowb[J - 1]) {
+            d = reinterpret_cast<T*>(sc.lds[J - 1] + rr * sc.rowb[J - 1] +
+                                     ((sc.head[J - 1] + rr * sc.hstep[J - 1]) & 15u)) +
+                (cout0 - sc.scol[J - 1]);
+        } else {
+            d = reinterpret_cast<T*>(base) + uint64_t(rr) * sc.stride[J - 1] +
+                (cout0 - sc.scol[J - 1]);
+        }
         // A lane's CO elements as one LDS vector write where they are whole
         // and aligned (every row of an aligned band): element writes put the
         // lanes 16 B apart for f32 level 1, a 4-way bank conflict (60% of
@@ -1097,6 +1112,15 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
             span[i] = p.dst[i] +
                       (uint64_t(f) * p.dst_frame_elems[i] + uint64_t(r0) * p.w[i] + c0) * sizeof(T);
             len[i] = rows * piece[i];
+            if (p.seg_rowwise) {
+                // misaligned rows: one LDS slot per row (StageCtx::rowb)
+                sc.head[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 15u);
+                sc.hstep[i] = (p.w[i] * uint32_t(sizeof(T))) & 15u;
+                sc.rowb[i] = (piece[i] + 30u) & ~15u;
+                sc.lds[i] = band_lds + off;
+                off += rows * sc.rowb[i];
+                continue;
+            }
             sc.head[i] = 0; // aligned frames: every piece starts on 16 bytes
         } else {
             sc.stride[i] = p.w[i];
@@ -1157,11 +1181,36 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         __syncthreads();
     }
 
-
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
         if (!((stage_mask >> i) & 1u) || len[i] == 0)
             continue;
+        if (sc.rowb[i]) {
+            // misaligned segment: row r's piece leaves in the 16-byte chunks
+            // of its own global span, whole ones as vectors, the two ends
+            // (shared with the neighbouring segments) byte by byte
+            const uint32_t cmax = sc.rowb[i] / 16u;
+            const uint32_t chunks = rows_of[i] * cmax;
+            const uint64_t pitch = uint64_t(p.w[i]) * sizeof(T);
+            for (uint32_t k = tid; k < chunks; k += nth) {
+                const uint32_t r = k / cmax, c = k - r * cmax;
+                const uint32_t h = (sc.head[i] + r * sc.hstep[i]) & 15u;
+                const uint32_t end = h + piece[i];
+                const uint32_t a = c * 16u, b = a + 16u;
+                if (a >= end)
+                    continue;
+                const uint8_t* l = sc.lds[i] + r * sc.rowb[i];
+                uint8_t* g = span[i] + r * pitch - h;
+                if (a >= h && b <= end) {
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(l + a);
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(g + a));
+                } else {
+                    for (uint32_t x = max(a, h); x < min(b, end); ++x)
+                        g[x] = l[x];
+                }
+            }
+            continue;
+        }
         if (seg_tiles) {
             // rows_of[i] pieces of piece[i] bytes, level pitch apart
             const uint32_t cpr = piece[i] / 16u;
@@ -1217,7 +1266,7 @@ band_lds_cap()
 // bands; 0 if no level is staged).
 inline uint32_t
 band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
-               uint32_t seg_cols = 0)
+               uint32_t seg_cols = 0, bool rowwise = false)
 {
     uint64_t total = 0;
     for (int i = 0; i < n_out; ++i) {
@@ -1225,7 +1274,10 @@ band_lds_bytes(size_t b, const LevelOut* outs, int n_out, uint32_t stage_mask,
             const uint64_t rows = uint64_t(1) << (n_out - i - 1);
             const uint64_t w = seg_cols ? std::min<uint64_t>(seg_cols >> (i + 1), outs[i].w)
                                         : outs[i].w;
-            total += (15 + rows * w * b + 15) & ~uint64_t(15);
+            if (rowwise)
+                total += rows * ((w * b + 30) & ~uint64_t(15)); // StageCtx::rowb slots
+            else
+                total += (15 + rows * w * b + 15) & ~uint64_t(15);
         }
     }
     return total > (1u << 30) ? (1u << 30) : uint32_t(total);
@@ -1957,6 +2009,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         static const int mis_max_env = int_env("AQZ_BAND_MIS_MAX", -1);
         const uint32_t mis_max = mis_max_env >= 0 ? uint32_t(std::min(mis_max_env, 8))
                                                   : (sizeof(T) == 2 ? 6u : 4u);
+        static const int mis_seg_env = std::min(int_env("AQZ_BAND_MIS_SEG", -1), 8);
         uint32_t stage_mask = 0;
         for (int i = 0; i < n_out; ++i) {
             const bool whole = (uint64_t(outs[i].w) * sizeof(T)) % 64 == 0 &&
@@ -2018,9 +2071,30 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             seg_tiles = 8;
             band_waves = 8;
             wide_max = 8;
+        } else if (misaligned && band_waves > mis_max &&
+                   (mis_seg_env > 0 ||
+                    (mis_seg_env < 0 && band_waves > 8 && (sizeof(T) == 2 || sizeof(T) == 4)))) {
+            // Misaligned bands of more than 8 tiles (2- and 4-byte types):
+            // balanced segments of at most 4 tiles ($AQZ_BAND_MIS_SEG: any
+            // band wider than one wave may store, segments of that many
+            // tiles; 0: never), each staged and stored by its last wave,
+            // every level row of a segment its own piece (StageCtx::rowb);
+            // only the pieces' ends share bursts with the neighbouring
+            // segments.  Same box, two rounds, against band workgroups with
+            // direct stores (profiles/r03/misaligned/mis_segments_ab*.log):
+            // f32 5472x3648 1264 -> 1092 us, 6000x4000 1167 -> 1104, 4100^2
+            // 1150 -> 1077; u16 6000x4000 585 -> 557, 5472x3648 534 -> 530.
+            // Narrower bands lost or tied (u16 4000x3000 557 -> 612 us, f32
+            // 3000^2 1099 -> 1428), and u8 gained only at exactly 6 tiles in
+            // 2-tile segments, so those keep direct stores.
+            const uint32_t mis_seg = mis_seg_env > 0 ? uint32_t(mis_seg_env) : 4u;
+            const uint32_t nseg = (p.units_x + mis_seg - 1) / mis_seg;
+            seg_tiles = (p.units_x + nseg - 1) / nseg;
+            band_waves = seg_tiles;
+            p.seg_rowwise = 1;
         }
         const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask,
-                                            seg_tiles * 64u * cols);
+                                            seg_tiles * 64u * cols, p.seg_rowwise != 0);
         const bool band = stage_mask && !band_off &&
                           band_waves <= wide_max && lds <= band_lds_cap() &&
                           total < (1ull << 31);

@@ -197,6 +197,10 @@ BATCH_GEOMETRIES = {
     # 10 px, so deep levels hold bursts shared by three waves
     "2d_complete_8tile": (halving_geometry(3900, 37, 4), 2, 1),
     "2d_complete_short_last": (halving_geometry(2570, 50, 4), 3, 1),
+    # misaligned bands of more than 8 tiles (u16 / f32: 10): balanced 4-tile
+    # segments, every level row its own LDS piece, stored by the segment's
+    # last wave; odd band at the bottom
+    "2d_mis_segments": (halving_geometry(4700, 41, 4), 2, 1),
 }
 
 
