@@ -402,8 +402,10 @@ int aqz_ds_run_device_batch(aqz_ds* ds,
  * overhang; when S > 1 every flag byte is written once by the wave that owns
  * it, so nothing is cleared first (S == 1: one byte per tile, cleared by a
  * fill before the kernel).
- * Pure-XY (2-D) pyramids only, frames at least one 16-byte load wide, no
- * input transposition; anything else is AQZ_INVALID_ARGUMENT.  Runs on
+ * Pure-XY (2-D) pyramids only, frames at least one 16-byte load wide (so
+ * is the first level of every later fused run: levels 4, 8, ... of deeper
+ * pyramids), no input transposition; anything else is AQZ_INVALID_ARGUMENT
+ * (aqz_ds_run_device_batch takes any width).  Runs on
  * `hip_stream` (NULL = the handle's stream) without synchronising;
  * `out_counts` as for aqz_ds_run_device_batch.  Pyramids deeper than 4
  * levels chain runs through handle scratch, so each tiled/chunked batch is
