@@ -819,7 +819,7 @@ struct StageCtx
     uint32_t hstep[kMaxFusedLevels];
 };
 
-template<typename T, int C, int J, int RO, int CO, bool EDGE>
+template<typename T, int C, int J, int RO, int CO, bool EDGE, bool ROWS = false>
 __device__ __forceinline__ void
 stage_level(const StageCtx& sc,
             const T (&out)[RO][CO],
@@ -845,7 +845,7 @@ stage_level(const StageCtx& sc,
             continue;
         const uint32_t rr = rout0 + r - (band_row0 >> J); // row within the band
         T* d;
-        if (sc.rowb[J - 1]) {
+        if constexpr (ROWS) {
             d = reinterpret_cast<T*>(sc.lds[J - 1] + rr * sc.rowb[J - 1] +
                                      ((sc.head[J - 1] + rr * sc.hstep[J - 1]) & 15u)) +
                 (cout0 - sc.scol[J - 1]);
@@ -888,7 +888,7 @@ stage_level(const StageCtx& sc,
 
 // Level J of the 2-D cascade: reduce, store, recurse to J+1.
 template<typename T, int M, int C, int J, int NL, int RI, int CI, bool EDGE,
-         bool NTS = false, bool STAGED = false, int TILED = 0>
+         bool NTS = false, int STAGED = 0, int TILED = 0>
 __device__ __forceinline__ void
 cascade_level(const CascadeParams& p,
               const T (&in)[RI][CI],
@@ -918,8 +918,9 @@ cascade_level(const CascadeParams& p,
     } else if constexpr (STAGED) {
         if ((sc->mask >> (J - 1)) & 1u) {
             // the band's rows start at row0 - row0 % 2^NL: one band per block
-            stage_level<T, C, J, RO, CO, EDGE>(*sc, out, p.w[J - 1], p.h[J - 1], col0, row0,
-                                               row0 & ~((1u << NL) - 1u), lane);
+            stage_level<T, C, J, RO, CO, EDGE, STAGED == 2>(*sc, out, p.w[J - 1], p.h[J - 1],
+                                                            col0, row0,
+                                                            row0 & ~((1u << NL) - 1u), lane);
         } else {
             store_level<T, C, J, RO, CO, EDGE, NTS>(dst, out, p.w[J - 1], p.h[J - 1],
                                                     col0, row0, lane);
@@ -943,7 +944,7 @@ cascade_level(const CascadeParams& p,
 // streams are marked non-temporal: measured on MI355X (tools/microbench.hip,
 // profiles/r01) the headline batch drops from ~530 to ~475 us with NT stores.
 template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true,
-         bool STAGED = false, int TILED = 0>
+         int STAGED = 0, int TILED = 0>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
@@ -1050,9 +1051,9 @@ cascade_kernel(CascadeParams p)
     const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
     // wave-uniform: interior tiles take the edge-free path
     if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
-        cascade_unit<T, M, NL, C, NT, false, true, false, TILED>(p, f, row0, col0, lane);
+        cascade_unit<T, M, NL, C, NT, false, true, 0, TILED>(p, f, row0, col0, lane);
     } else {
-        cascade_unit<T, M, NL, C, NT, true, true, false, TILED>(p, f, row0, col0, lane);
+        cascade_unit<T, M, NL, C, NT, true, true, 0, TILED>(p, f, row0, col0, lane);
     }
 }
 
@@ -1071,7 +1072,7 @@ cascade_kernel(CascadeParams p)
 // is split into segments of seg_tiles tiles, one workgroup each, every level
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
-template<typename T, int M, int NL, int C, bool NT = true>
+template<typename T, int M, int NL, int C, bool NT = true, bool ROWS = false>
 __global__ __launch_bounds__(512) void
 cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
 {
@@ -1112,7 +1113,7 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
             span[i] = p.dst[i] +
                       (uint64_t(f) * p.dst_frame_elems[i] + uint64_t(r0) * p.w[i] + c0) * sizeof(T);
             len[i] = rows * piece[i];
-            if (p.seg_rowwise) {
+            if constexpr (ROWS) {
                 // misaligned rows: one LDS slot per row (StageCtx::rowb)
                 sc.head[i] = uint32_t(reinterpret_cast<uintptr_t>(span[i]) & 15u);
                 sc.hstep[i] = (p.w[i] * uint32_t(sizeof(T))) & 15u;
@@ -1150,9 +1151,9 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
         const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
         if (interior)
-            cascade_unit<T, M, NL, C, NT, false, true, true>(p, f, row0, col0, lane, &sc);
+            cascade_unit<T, M, NL, C, NT, false, true, ROWS ? 2 : 1>(p, f, row0, col0, lane, &sc);
         else
-            cascade_unit<T, M, NL, C, NT, true, true, true>(p, f, row0, col0, lane, &sc);
+            cascade_unit<T, M, NL, C, NT, true, true, ROWS ? 2 : 1>(p, f, row0, col0, lane, &sc);
     }
     uint32_t tid = threadIdx.x, nth = blockDim.x;
     if (last_mode) {
@@ -1185,7 +1186,7 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
     for (int i = 0; i < NL; ++i) {
         if (!((stage_mask >> i) & 1u) || len[i] == 0)
             continue;
-        if (sc.rowb[i]) {
+        if constexpr (ROWS) {
             // misaligned segment: row r's piece leaves in the 16-byte chunks
             // of its own global span, whole ones as vectors, the two ends
             // (shared with the neighbouring segments) byte by byte
@@ -2071,13 +2072,12 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             seg_tiles = 8;
             band_waves = 8;
             wide_max = 8;
-        } else if (misaligned && band_waves > mis_max &&
-                   (mis_seg_env > 0 ||
-                    (mis_seg_env < 0 && band_waves > 8 && (sizeof(T) == 2 || sizeof(T) == 4)))) {
-            // Misaligned bands of more than 8 tiles (2- and 4-byte types):
-            // balanced segments of at most 4 tiles ($AQZ_BAND_MIS_SEG: any
-            // band wider than one wave may store, segments of that many
-            // tiles; 0: never), each staged and stored by its last wave,
+        } else if (misaligned && band_waves > mis_max && (sizeof(T) == 2 || sizeof(T) == 4) &&
+                   cols == CW && (mis_seg_env > 0 || (mis_seg_env < 0 && band_waves > 8))) {
+            // Misaligned bands of more than 8 tiles (2- and 4-byte types, wide
+            // tiles): balanced segments of at most 4 tiles
+            // ($AQZ_BAND_MIS_SEG: any band of those types wider than one
+            // wave may store, segments of that many tiles; 0: never), each staged and stored by its last wave,
             // every level row of a segment its own piece (StageCtx::rowb);
             // only the pieces' ends share bursts with the neighbouring
             // segments.  Same box, two rounds, against band workgroups with
@@ -2123,40 +2123,37 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                 constexpr bool NT = decltype(nttag)::value;
                 if (band) {
                     const dim3 blk(64 * band_waves);
-                    switch (n_out) {
-                        case 1:
+                    auto launch_band = [&](auto rtag) {
+                        constexpr bool RW = decltype(rtag)::value;
+                        auto one = [&](auto ltag) {
+                            constexpr int NLV = decltype(ltag)::value;
                             if (lds > 65536) // above the default per-workgroup LDS
                                 (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 1, C, NT>),
+                                  reinterpret_cast<const void*>(
+                                    &cascade_band_kernel<T, M, NLV, C, NT, RW>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 1, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
-                            break;
-                        case 2:
-                            if (lds > 65536) // above the default per-workgroup LDS
-                                (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 2, C, NT>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 2, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
-                            break;
-                        case 3:
-                            if (lds > 65536) // above the default per-workgroup LDS
-                                (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 3, C, NT>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 3, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
-                            break;
-                        default:
-                            if (lds > 65536) // above the default per-workgroup LDS
-                                (void)hipFuncSetAttribute(
-                                  reinterpret_cast<const void*>(&cascade_band_kernel<T, M, 4, C, NT>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, 4, C, NT>), dim3(bands), blk,
-                                               lds, stream, p, stage_mask, seg_tiles);
-                            break;
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, NLV, C, NT, RW>),
+                                               dim3(bands), blk, lds, stream, p, stage_mask,
+                                               seg_tiles);
+                        };
+                        switch (n_out) {
+                            case 1: one(std::integral_constant<int, 1>{}); break;
+                            case 2: one(std::integral_constant<int, 2>{}); break;
+                            case 3: one(std::integral_constant<int, 3>{}); break;
+                            default: one(std::integral_constant<int, 4>{}); break;
+                        }
+                    };
+                    // misaligned segments: a separate instantiation, so that
+                    // whole bands keep their code (a runtime branch per row
+                    // cost 3000^2 / 2600^2 u16 8-9%), for 2- and 4-byte types
+                    // at the wide tile only (where the launcher picks them)
+                    if constexpr ((sizeof(T) == 2 || sizeof(T) == 4) && C == int(CW)) {
+                        if (p.seg_rowwise) {
+                            launch_band(std::true_type{});
+                            return;
+                        }
                     }
+                    launch_band(std::false_type{});
                     return;
                 }
                 switch (n_out) {
