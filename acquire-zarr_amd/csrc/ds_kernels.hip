@@ -1073,7 +1073,14 @@ cascade_kernel(CascadeParams p)
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
 template<typename T, int M, int NL, int C, bool NT = true, bool ROWS = false>
-__global__ __launch_bounds__(512) void
+__global__ __launch_bounds__(512)
+// 2-byte Min / Max on line-aligned rows (NT loads): held to 80 VGPRs, 6
+// waves per SIMD instead of 5 at 81 (headline Min 481 -> 470 us, Max 483
+// -> 470); the same hint on misaligned bands stored by their last wave cost
+// 3000^2 Max 546 -> 584 us, and Mean would spill at 80
+// (profiles/r03/occupancy/)
+__attribute__((amdgpu_waves_per_eu(
+  sizeof(T) == 2 && (M == kMin || M == kMax) && NT ? 6 : 1))) void
 cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t band_lds[];
