@@ -2060,17 +2060,29 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
             stage_mask = all_levels;
             wide_max = 8;
-            // 8-tile bands go in two 4-tile segments: a whole 4096 f32 band
+            // 8-tile bands go in segments (first measured as two of 4 tiles,
+            // below): a whole 4096 f32 band
             // needs 85 KiB of LDS, one workgroup per CU, whose loads and
             // stores then never overlap; segments fit two or three.  Same
             // box, two rounds (profiles/r03/f32/band_seg4_ab.log): f32 Max
             // 1062 -> 999 us, Mean 1042 -> 991, Min 1064 -> 998, the headline
             // 478 -> 473; 6-tile bands lost (3072^2 470 -> 510), so only
             // bands of 8.  $AQZ_BAND_SEG4=0 / 1: never / always.
+            // Tiles per segment: 3 (segments of 3, 3, 2) for 2-byte Mean and
+            // for Decimate, 4 otherwise.  Same box, two rounds each
+            // (profiles/r03/f32/segment_tiles_ab*.log): headline (u16 Mean)
+            // 473-475 -> 462-463 us, 4096x2160 469-473 -> 461-462, u16
+            // Decimate 297 -> 294, f32 Decimate 644-652 -> 607-608; but u16
+            // Min/Max 472-474 -> 480-483 and f32 Mean/Min/Max 990-1000 ->
+            // 1027-1030, which keep 4.  $AQZ_BAND_SEGN overrides (A/B).
             static const int seg4 = int_env("AQZ_BAND_SEG4", -1);
+            static const int segn_env = int_env("AQZ_BAND_SEGN", 0);
+            const uint32_t segn = segn_env > 0 ? uint32_t(std::min(segn_env, 8))
+                                  : (method == kDecimate || (method == kMean && sizeof(T) == 2))
+                                    ? 3u : 4u;
             if (seg4 == 1 || (seg4 < 0 && band_waves == 8)) {
-                seg_tiles = 4;
-                band_waves = 4;
+                seg_tiles = segn;
+                band_waves = segn;
             }
         } else if (band_aligned && band_segments && stage_mask == 0 && band_waves > 8 &&
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels, 8u * 64u * cols) <=
