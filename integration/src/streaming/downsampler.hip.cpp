@@ -14,6 +14,10 @@
 //   take_frame_tiled(level, t)   new -> aqz_ds_take_frame_tiled
 //   level_is_tiled(level)        new
 //
+// take_frame on a level the add's background job already took tiled untiles
+// that copy on the host; add_frame_async settles a previous pending one
+// before it reuses the take buffers.
+//
 // The rest of the class stays in the reference's downsampler.cpp, compiled
 // unchanged: acquire-zarr-hip.patch only puts the CPU constructor, add_frame,
 // take_frame, emplace_downsampled_frame_ and the scalar kernels they use
@@ -34,6 +38,8 @@
 
 #include "aqz_downsampler.h"
 
+#include <algorithm>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -134,6 +140,12 @@ zarr::Downsampler::add_frame(std::vector<uint8_t>& frame)
 void
 zarr::Downsampler::add_frame_async(std::vector<uint8_t>& frame)
 {
+    // A previous add_frame_async may still be running its takes into takes_
+    // and taken_: settle it (which also marks the levels it took as held)
+    // before either is touched.
+    if (pending_) {
+        wait();
+    }
     // The takes write_multiscale_frames_ makes right after the add
     // (multiscale.array.cpp:298-325) run in the same background job, so the
     // levels' device-to-host copies overlap level 0's chunking too.  A level
@@ -200,6 +212,34 @@ zarr::Downsampler::hand_over_(int level, std::vector<uint8_t>& out)
     return true;
 }
 
+void
+zarr::Downsampler::untile_held_(int level, std::vector<uint8_t>& out)
+{
+    // taken_[level] holds the frame chunk-tiled (tile t = ty * n_tiles_x + tx,
+    // tile_rows x tile_cols, row-major, zero overhang); take_frame hands it
+    // out row-major, as the reference's cached frame would be.
+    const auto [tile_rows, tile_cols] = tiles_[level];
+    const auto& dims = writer_configurations_.at(level)->dimensions;
+    const size_t w = dims->width_dim().array_size_px;
+    const size_t h = dims->height_dim().array_size_px;
+    const size_t bpp = aqz_ds_level_bytes(gpu_, uint32_t(level)) / (w * h);
+    const size_t ntx = (w + tile_cols - 1) / tile_cols;
+    const uint8_t* tiles = taken_[level].data();
+    out.resize(w * h * bpp);
+    for (size_t y = 0; y < h; ++y) {
+        const size_t ty = y / tile_rows, r = y % tile_rows;
+        for (size_t tx = 0; tx < ntx; ++tx) {
+            const size_t x0 = tx * tile_cols;
+            const size_t n = std::min<size_t>(tile_cols, w - x0);
+            const size_t t = ty * ntx + tx;
+            std::memcpy(out.data() + (y * w + x0) * bpp,
+                        tiles + ((t * tile_rows + r) * tile_cols) * bpp,
+                        n * bpp);
+        }
+    }
+    holding_[level] = 0;
+}
+
 bool
 zarr::Downsampler::take_frame(int level, std::vector<uint8_t>& frame_data)
 {
@@ -211,8 +251,13 @@ zarr::Downsampler::take_frame(int level, std::vector<uint8_t>& frame_data)
     if (pending_) {
         wait();
     }
-    if (!level_is_tiled(level) && hand_over_(level, frame_data)) {
-        return true; // taken in the add's background job
+    if (holding_[level]) {
+        // taken in the add's background job; a tiled level took it tiled
+        if (level_is_tiled(level)) {
+            untile_held_(level, frame_data);
+            return true;
+        }
+        return hand_over_(level, frame_data);
     }
     // Size query first: the frame stays cached until it is copied out.
     size_t nbytes = 0;

@@ -99,10 +99,23 @@ oracle_bytes_of_type(int dtype)
         return (T)(s / 2);                                                     \
     }
 
-/* Floating point: left-to-right sum in T, then divide. */
+/* Floating point: left-to-right sum in T, then divide.
+ *
+ * NaN payloads: C leaves them open, and a compiler may commute `x + y`.  The
+ * reference's compiled mean2/mean4 (g++ -O3 -mavx2, oracle/_ref) evaluate
+ * `vaddss y, x` with the LEFT operand as the first source, so when both
+ * operands are NaN the left one's (quieted) payload survives (Intel SDM
+ * vol. 1 table 4-7).  add_<T> pins that order: with two NaNs it returns
+ * x + x, whose payload is x's whatever operand order the compiler picks; with
+ * one NaN or none the order cannot change the result.  Pinned against the
+ * reference by tests/test_reference_pin.py (Z-pair Mean over NaN planes). */
 #define MEAN_FLOAT(T)                                                          \
-    static T mean4_##T(T a, T b, T c, T d) { return (((a + b) + c) + d) / 4; } \
-    static T mean2_##T(T a, T b) { return (a + b) / 2; }
+    static T add_##T(T x, T y) { return (x != x && y != y) ? x + x : x + y; }  \
+    static T mean4_##T(T a, T b, T c, T d)                                     \
+    {                                                                          \
+        return add_##T(add_##T(add_##T(a, b), c), d) / 4;                      \
+    }                                                                          \
+    static T mean2_##T(T a, T b) { return add_##T(a, b) / 2; }
 
 typedef float float32_t;
 typedef double float64_t;

@@ -6,18 +6,20 @@ is mix(seed + (k * N + i + 1) * 0x9E3779B97F4A7C15), N = pixels per frame.
 Integers take the low bits; float32 takes the top 24 bits scaled to
 [-1000, 1000).  Both the oracle (CPU tests) and the
 HIP path (GPU tests) are checked against the SHA-256 of every level's frames,
-concatenated in emit order, committed in tests/golden/config_digests.json by
-tests/golden/make_digests.py.  The digests were made with the oracle, so they
-pin the HIP path and guard the oracle against regressions; the oracle itself
-is pinned by the reference's KATs (tests/test_oracle_kats.py).
+concatenated in emit order.  GOLDEN, tests/golden/reference_digests.json, was
+made by the REFERENCE ITSELF (oracle/_ref: downsampler.cpp compiled
+unmodified; tests/golden/make_reference_vectors.py --digests).  The oracle's
+own digests (tests/golden/config_digests.json, tests/golden/make_digests.py)
+must equal them (tests/test_reference_pin.py).
 """
 import hashlib
 import os
 
 import numpy as np
 
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
-                      "config_digests.json")
+_GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+GOLDEN = os.path.join(_GOLDEN_DIR, "reference_digests.json")      # made by the reference
+ORACLE_DIGESTS = os.path.join(_GOLDEN_DIR, "config_digests.json")  # made by the oracle
 SEED = 0xA0C2A11
 SPACE, TIME = 0, 2
 

@@ -37,7 +37,7 @@ def main():
             entry["methods"][mname] = du.run_stream(make_oracle, name, m)
             print(name, mname, entry["methods"][mname], flush=True)
         out["configs"][name] = entry
-    with open(du.GOLDEN, "w") as f:
+    with open(du.ORACLE_DIGESTS, "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")
 

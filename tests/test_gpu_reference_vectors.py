@@ -1,0 +1,82 @@
+"""GPU parity against vectors made by the REFERENCE ITSELF
+(tests/golden/reference_vectors.{npz,json}: acquire-zarr v0.8.1's
+zarr::Downsampler compiled unmodified, tests/golden/make_reference_vectors.py).
+
+* the streaming drop-in (aqz_ds_add_frame / aqz_ds_take_frame) replays all
+  320 cases — 8 geometries x 10 dtypes x 4 methods — frame by frame, with the
+  reference's frame readiness, untaken frames and odd-Z pass-through;
+* the device batch (aqz_ds_run_device_batch, the bench path) reproduces each
+  level's frames of every geometry whose levels are all taken after every
+  frame.
+
+Integers bit-exact; floats bit-exact on every non-NaN value with NaN
+positions equal (NaN payloads are not compared: refvec.same).  No reference
+code runs here — the fixtures travel, the reference does not.
+"""
+import numpy as np
+import pytest
+
+import refvec as rv
+from gpu_util import empty_device, from_device, launch_stream, to_device, torch_cuda
+
+pytestmark = pytest.mark.gpu
+
+MAN, VEC = rv.load()
+CASES = rv.cases(MAN)
+IDS = [f"{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in CASES]
+
+
+@pytest.mark.parametrize("geom,dtype,method", CASES, ids=IDS)
+def test_stream_replays_reference_vectors(aqz, geom, dtype, method):
+    handles = []
+
+    def make(dims, dt, m):
+        ds = aqz.Downsampler(aqz.level_geometry(aqz.plan_levels(dims)), dt, m)
+        handles.append(ds)
+        return ds
+    try:
+        rv.replay(make, MAN, VEC, geom, dtype, method, nan_bits=False)
+    finally:
+        for ds in handles:
+            ds.close()
+
+
+BATCH_CASES = [(g, d, m) for g, d, m in CASES if MAN["geometries"][g]["take"] == "all"]
+
+
+@pytest.mark.parametrize("geom,dtype,method", BATCH_CASES,
+                         ids=[f"{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in BATCH_CASES])
+def test_device_batch_reproduces_reference_levels(aqz, geom, dtype, method):
+    torch = torch_cuda()
+    g = MAN["geometries"][geom]
+    dt = np.dtype(dtype)
+    frames = VEC[f"in/{geom}/{dtype}"]
+    name = f"{geom}/{dtype}/{rv.METHOD_NAMES[method]}"
+    ev, out = VEC[f"ev/{name}"], VEC[f"out/{name}"]
+    # the reference's frames per level, in emit order
+    want = {L: [] for L in range(1, len(g["levels"]))}
+    off = 0
+    for k, L, has, nb in ev:
+        if has:
+            want[int(L)].append(out[off:off + nb])
+            off += int(nb)
+    geo = [tuple(x) for x in g["geometry"]]
+    n = frames.shape[0]
+    bpp = dt.itemsize
+    d_in = to_device(frames)
+    outs = [None] + [empty_device(n * w * h * bpp) for w, h, _ in geo[1:]]
+    ds = aqz.Downsampler(geo, dt, method)
+    try:
+        counts = ds.run_device_batch(d_in.data_ptr(), n, [0] + [o.data_ptr() for o in outs[1:]],
+                                     launch_stream())
+        torch.cuda.synchronize()
+    finally:
+        ds.close()
+    for L, frames_L in want.items():
+        w, h, _ = geo[L]
+        assert counts[L] == len(frames_L), f"{name}: level {L} frames"
+        got = from_device(outs[L], np.uint8, (-1,))[:len(frames_L) * w * h * bpp]
+        for k, wb in enumerate(frames_L):
+            gb = got[k * w * h * bpp:(k + 1) * w * h * bpp]
+            bad = rv.same(gb, wb, dt, nan_bits=False)
+            assert bad is None, f"{name}: level {L} frame {k}: {bad.size} elements differ"

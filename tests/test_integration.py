@@ -25,11 +25,14 @@ src/streaming sources.  Then:
   — the oracle's tiling placed by the oracle's KAT-pinned addressing — on
   ragged frames, several layers and N-D chunk lattices.
 
-nlohmann/json and google/crc32c are not in this image, so
-tests/integration/nlohmann/json.hpp and tests/integration/crc32c/crc32c.h are
-compile-only stand-ins: nothing built with them is linked or run.  blosc.h and
-zstd.h are the image's own (/opt/conda/include).  Skipped when /root/reference
-is absent (the GPU box)."""
+nlohmann/json is the image's genuine 3.1.1 (/opt/conda/include/json.hpp,
+reached as <nlohmann/json.hpp> through a symlink); blosc.h and zstd.h are the
+image's own (/opt/conda/include).  google/crc32c is not in this image:
+tests/integration/crc32c/crc32c.h declares its one entry point so the patched
+array.cpp can be syntax-checked, and nothing built with it is linked or run.
+The adapter itself is linked here and EXECUTED on the GPU by
+tests/test_gpu_adapter.py (tests/integration/build_adapter_harness.sh).
+Skipped when /root/reference is absent (the GPU box)."""
 import os
 import shutil
 import subprocess
@@ -42,6 +45,7 @@ STUB = os.path.join(ROOT, "tests", "integration")
 LIB_DIR = os.path.join(ROOT, "acquire-zarr_amd")
 CONDA_INC = "/opt/conda/include"   # blosc.h, zstd.h (part of the image)
 CONDA_LIB = "/opt/conda/lib"
+JSON_HPP = "/opt/conda/include/json.hpp"  # nlohmann/json 3.1.1, part of the image
 
 pytestmark = pytest.mark.skipif(
     not os.path.exists(os.path.join(REF, "src", "streaming", "downsampler.hh")),
@@ -51,6 +55,9 @@ pytestmark = pytest.mark.skipif(
 @pytest.fixture(scope="module")
 def tree(tmp_path_factory):
     t = tmp_path_factory.mktemp("acquire-zarr")
+    inc = t / "_json_inc" / "nlohmann"
+    inc.mkdir(parents=True)
+    os.symlink(JSON_HPP, inc / "json.hpp")
     for d in ("include", "cmake", os.path.join("src", "streaming"), os.path.join("src", "logger")):
         shutil.copytree(os.path.join(REF, d), t / d)
     shutil.copy(os.path.join(REF, "CMakeLists.txt"), t / "CMakeLists.txt")
@@ -65,7 +72,7 @@ def gxx(tree, args, defines=("AQZ_DOWNSAMPLER_HIP",)):
     cmd = ["g++", "-std=c++20", "-fPIC", "-Wall", "-Wno-unknown-pragmas",
            "-Wno-sign-compare", "-Wno-unused-variable"]
     cmd += [f"-D{d}" for d in defines]
-    cmd += ["-I", STUB, "-I", os.path.join(ROOT, "include"),
+    cmd += ["-I", str(tree / "_json_inc"), "-I", STUB, "-I", os.path.join(ROOT, "include"),
             "-I", str(tree / "include"), "-I", str(tree / "src" / "streaming"),
             "-I", str(tree / "src" / "logger"), "-idirafter", CONDA_INC] + list(args)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -105,6 +112,7 @@ def test_adapter_links_against_the_c_abi(tree, tmp_path):
     srcs = [tree / "src" / "streaming" / "downsampler.cpp",
             tree / "src" / "streaming" / "downsampler.hip.cpp",
             tree / "src" / "streaming" / "array.dimensions.cpp",
+            tree / "src" / "streaming" / "zarr.common.cpp",
             tree / "src" / "logger" / "logger.cpp"]
     objs = []
     for s in srcs:
@@ -112,12 +120,17 @@ def test_adapter_links_against_the_c_abi(tree, tmp_path):
         gxx(tree, ["-O1", "-c", str(s), "-o", str(o)])
         objs.append(str(o))
     # Every symbol the adapter needs resolves in libaqz_downsampler.so, the
-    # reference's own objects or the C/C++ runtime.  The only exceptions are
-    # three zarr.common.cpp helpers that array.dimensions.cpp calls; that file
-    # includes blosc.h and zstd.h, which this image lacks.
+    # reference's own objects, the image's c-blosc / zstd or the C/C++ runtime.
+    libs = tmp_path / "lib"
+    libs.mkdir()
+    for name in ("libblosc.so.1", "liblz4.so.1", "libz.so.1", "libzstd.so.1"):
+        shutil.copy(os.path.join(CONDA_LIB, name), libs / name)
+    os.symlink("libblosc.so.1", libs / "libblosc.so")
+    os.symlink("libzstd.so.1", libs / "libzstd.so")
     so = tmp_path / "libzarr_downsampler_hip.so"
     gxx(tree, ["-shared", "-o", str(so)] + objs +
         ["-L", LIB_DIR, "-laqz_downsampler", f"-Wl,-rpath,{LIB_DIR}",
+         "-L", str(libs), "-lblosc", "-lzstd", f"-Wl,-rpath,{libs}",
          "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
     undef = subprocess.run(["nm", "-DC", "--undefined-only", str(so)],
                            capture_output=True, text=True, check=True).stdout.splitlines()
@@ -132,10 +145,10 @@ def test_adapter_links_against_the_c_abi(tree, tmp_path):
         if name.startswith("aqz_"):
             assert name in exported, f"{name} not exported by libaqz_downsampler.so"
             continue
+        if name.startswith(("blosc_", "ZSTD_")):
+            continue
         unresolved.add(name)
-    assert unresolved <= {"zarr::bytes_of_type(ZarrDataType)",
-                          "zarr::chunks_along_dimension(ZarrDimension const&)",
-                          "zarr::shards_along_dimension(ZarrDimension const&)"}, unresolved
+    assert not unresolved, unresolved
     nm = "\n".join(undef)
     for sym in ("aqz_ds_create", "aqz_ds_add_frame", "aqz_ds_add_frame_async_take",
                 "aqz_ds_wait", "aqz_ds_take_frame", "aqz_ds_take_frame_tiled",
@@ -146,7 +159,7 @@ def test_adapter_links_against_the_c_abi(tree, tmp_path):
     for m in ("zarr::Downsampler::Downsampler(", "zarr::Downsampler::~Downsampler()",
               "zarr::Downsampler::add_frame(", "zarr::Downsampler::take_frame(",
               "zarr::Downsampler::add_frame_async(", "zarr::Downsampler::take_frame_tiled(",
-              "zarr::Downsampler::get_metadata() const",
+              "zarr::Downsampler::get_metadata",
               "zarr::Downsampler::writer_configurations() const"):
         assert m in defined, m
 
