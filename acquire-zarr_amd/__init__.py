@@ -47,6 +47,8 @@ EXPORTS = (
     "aqz_ds_device",
     "aqz_ds_last_error", "aqz_last_error", "aqz_method_name",
     "aqz_method_metadata_json", "aqz_version",
+    "aqz_shard_unit", "aqz_node_create", "aqz_node_destroy", "aqz_node_handle_count",
+    "aqz_node_handle", "aqz_node_run_host_batch", "aqz_node_last_error",
 )
 
 
@@ -193,6 +195,19 @@ def lib() -> ctypes.CDLL:
     L.aqz_method_metadata_json.restype = ctypes.c_char_p
     L.aqz_version.argtypes = []
     L.aqz_version.restype = ctypes.c_char_p
+    L.aqz_shard_unit.argtypes = [ctypes.POINTER(LevelDesc), u32, ctypes.POINTER(u32),
+                                 ctypes.POINTER(u32)]
+    L.aqz_node_create.argtypes = [ctypes.POINTER(LevelDesc), u32, i32, i32,
+                                  ctypes.POINTER(i32), u32, ctypes.POINTER(vp)]
+    L.aqz_node_destroy.argtypes = [vp]
+    L.aqz_node_destroy.restype = None
+    L.aqz_node_handle_count.argtypes = [vp]
+    L.aqz_node_handle_count.restype = u32
+    L.aqz_node_handle.argtypes = [vp, u32]
+    L.aqz_node_handle.restype = vp
+    L.aqz_node_run_host_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u32)]
+    L.aqz_node_last_error.argtypes = [vp]
+    L.aqz_node_last_error.restype = ctypes.c_char_p
     _lib = L
     return L
 
@@ -693,3 +708,62 @@ def alg_bytes_per_frame(geometry, bpp: int) -> int:
     for w, h, _ in geometry[1:]:
         total += w * h * bpp
     return total
+
+
+def shard_unit(geometry):
+    """(unit, frames emitted per level per unit) of a pyramid (aqz_shard_unit):
+    the slab of level-0 frames a node deals to one GPU at a time."""
+    n = len(geometry)
+    desc = (LevelDesc * n)(*[LevelDesc(*g) for g in geometry])
+    u = ctypes.c_uint32(0)
+    per = (ctypes.c_uint32 * n)()
+    L = lib()
+    rc = L.aqz_shard_unit(desc, n, ctypes.byref(u), per)
+    if rc:
+        raise AqzError(rc, L.aqz_last_error().decode())
+    return u.value, list(per)
+
+
+class Node:
+    """Binding of an ``aqz_node``: frames sharded over `devices` (SURVEY
+    §8(e)); run_host_batch returns each level in frame-id order."""
+
+    def __init__(self, geometry, dtype, method: int, devices):
+        self.dtype = np.dtype(dtype)
+        self.geometry = [tuple(int(x) for x in g) for g in geometry]
+        n = len(self.geometry)
+        desc = (LevelDesc * n)(*[LevelDesc(*g) for g in self.geometry])
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        L = lib()
+        rc = L.aqz_node_create(desc, n, dtype_code(self.dtype), method, devs, len(devices),
+                               ctypes.byref(h))
+        if rc:
+            raise AqzError(rc, L.aqz_last_error().decode())
+        self._h = h
+        self.unit, self.frames_per_unit = shard_unit(self.geometry)
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().aqz_node_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def handle_devices(self):
+        L = lib()
+        return [L.aqz_ds_device(L.aqz_node_handle(self._h, i))
+                for i in range(L.aqz_node_handle_count(self._h))]
+
+    def run_host_batch(self, host_frames: int, n_frames: int, host_outs):
+        """host_frames / host_outs[L] are host addresses (index 0 ignored)."""
+        n = len(self.geometry)
+        outs = (ctypes.c_void_p * n)(*([None] + [int(p) for p in host_outs[1:]]))
+        counts = (ctypes.c_uint32 * n)()
+        L = lib()
+        rc = L.aqz_node_run_host_batch(self._h, host_frames, n_frames, outs, counts)
+        if rc:
+            raise AqzError(rc, L.aqz_node_last_error(self._h).decode())
+        return list(counts)

@@ -592,6 +592,10 @@ aqz_blosc_compress_device(aqz_blosc_ctx* ctx, int clevel, int shuffle, uint32_t 
         for (auto& t : pool)
             t.join();
         if (failed.load() != AQZ_OK) {
+            // the later groups' copies into ctx->h_filtered may still be
+            // queued: drain `stream` here (Drain does it again on the way
+            // out) so the ctx can be reused or destroyed at once
+            (void)hipStreamSynchronize(stream);
             aqz::set_last_error("blosc_compress_device: staged copy failed");
             return failed.load();
         }

@@ -1,0 +1,304 @@
+// ds_node.cpp — frame sharding over the GPUs of one node.
+//
+// An aqz_node is one aqz_ds handle per entry of `devices` (entries may repeat
+// an ordinal: two handles on one GPU).  Frames are independent work units
+// once the Z pairing is respected, so a host batch is cut into contiguous
+// blocks of whole SHARD UNITS, one block per handle, and every handle runs
+// the pipelined host batch (aqz_ds_run_host_batch: its own streams, its own
+// PCIe link) on its block in its own host thread.  Each block writes its
+// levels straight to the place its frames hold in the batch's outputs, so
+// the caller gets every level in frame-id order — the order
+// Array::write_frame insists on (array.cpp:179-189) — with no re-sequencing
+// pass and no collective.
+//
+// Shard unit: the fewest level-0 frames after which add_frame's state
+// (downsampler.cpp:306-401: partial Z planes, level_frame_count_ modulo an
+// odd plane count) is back where a fresh handle starts, so a fresh handle
+// fed a block from a unit boundary emits exactly what one handle fed the
+// whole stream would.
+//   * no level halves Z: 1 frame;
+//   * h levels halve Z and the stack's planes P divide by 2^h: 2^h planes
+//     (every intermediate plane count is even, so no plane passes through);
+//   * otherwise: the whole stack, P planes.
+// aqz_shard_unit checks the unit by running add_frame's control flow
+// (counts only) over one unit from a fresh state.
+#include "aqz_downsampler.h"
+#include "abi_guard.hh"
+#include "ds_kernels.hh"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+struct aqz_node
+{
+    std::vector<aqz_ds*> ds;
+    std::vector<aqz_level_desc> lv;
+    std::vector<size_t> bytes;      // one frame per level
+    uint32_t unit = 1;              // level-0 frames per shard unit
+    std::vector<uint32_t> per_unit; // frames each level emits per unit
+    uint64_t frames = 0;            // level-0 frames taken so far
+    std::string err;
+};
+
+namespace aqz {
+
+inline std::string*
+abi_err_slot(aqz_node* n)
+{
+    return n ? &n->err : nullptr;
+}
+
+} // namespace aqz
+
+namespace {
+
+// add_frame's control flow with the pixels left out (downsampler.cpp:
+// 306-401, emplace :599-605): which levels emit a frame.  `count` and
+// `partial` carry the state between frames.
+void
+count_frame(const std::vector<aqz_level_desc>& lv,
+            std::vector<uint64_t>& count,
+            std::vector<uint8_t>& partial,
+            std::vector<uint32_t>& emitted)
+{
+    ++count[0];
+    for (size_t L = 1; L < lv.size(); ++L) {
+        const uint32_t prev_planes = lv[L - 1].planes, next_planes = lv[L].planes;
+        bool average = next_planes < prev_planes;
+        if (prev_planes % 2 != 0 && count[L - 1] % prev_planes == 0)
+            average = false;
+        if (average && !partial[L]) {
+            partial[L] = 1;
+            return;
+        }
+        partial[L] = 0;
+        ++count[L];
+        ++emitted[L];
+    }
+}
+
+int
+fail(aqz_node* n, int rc, const std::string& what)
+{
+    n->err = what;
+    return rc;
+}
+
+} // namespace
+
+extern "C" {
+
+int
+aqz_shard_unit(const aqz_level_desc* levels,
+               uint32_t n_levels,
+               uint32_t* unit,
+               uint32_t* frames_per_unit)
+{
+    try {
+        if (!levels || n_levels == 0 || n_levels > AQZ_MAX_LEVELS || !unit) {
+            aqz::set_last_error("shard_unit: bad arguments");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        uint32_t halvings = 0;
+        for (uint32_t L = 1; L < n_levels; ++L)
+            halvings += levels[L].planes < levels[L - 1].planes;
+        const uint32_t planes = levels[0].planes;
+        uint32_t u = 1;
+        if (halvings > 0)
+            u = (halvings < 32 && planes % (1u << halvings) == 0) ? (1u << halvings) : planes;
+        if (u == 0) {
+            aqz::set_last_error("shard_unit: Z halves but level 0 has no planes");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        // one unit from a fresh state must leave it fresh again: no stored
+        // plane, and every count the odd-stack pass-through reads (level L's
+        // when L has an odd plane count and L+1 halves Z) at a multiple of
+        // that plane count
+        std::vector<aqz_level_desc> lv(levels, levels + n_levels);
+        std::vector<uint64_t> count(n_levels, 0);
+        std::vector<uint8_t> partial(n_levels, 0);
+        std::vector<uint32_t> emitted(n_levels, 0);
+        for (uint32_t f = 0; f < u; ++f)
+            count_frame(lv, count, partial, emitted);
+        emitted[0] = u;
+        for (uint32_t L = 0; L < n_levels; ++L) {
+            bool fresh = !partial[L];
+            if (L + 1 < n_levels && levels[L].planes % 2 != 0 &&
+                levels[L + 1].planes < levels[L].planes)
+                fresh = fresh && count[L] % levels[L].planes == 0;
+            if (!fresh) {
+                aqz::set_last_error("shard_unit: no shard unit restores the Z-pairing state");
+                return AQZ_INVALID_ARGUMENT;
+            }
+        }
+        *unit = u;
+        if (frames_per_unit)
+            std::copy(emitted.begin(), emitted.end(), frames_per_unit);
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
+    }
+}
+
+int
+aqz_node_create(const aqz_level_desc* levels,
+                uint32_t n_levels,
+                int dtype,
+                int method,
+                const int* devices,
+                uint32_t n_devices,
+                aqz_node** out)
+{
+    try {
+        if (!out) {
+            aqz::set_last_error("node_create: null output handle");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        *out = nullptr;
+        if (!devices || n_devices == 0 || n_devices > 64) {
+            aqz::set_last_error("node_create: need 1..64 device entries");
+            return AQZ_INVALID_ARGUMENT;
+        }
+        // the reference's order: dtype, then method (downsampler.cpp:293-303)
+        if (!aqz::dtype_valid(dtype)) {
+            aqz::set_last_error("Invalid data type: " + std::to_string(dtype));
+            return AQZ_INVALID_ARGUMENT;
+        }
+        if (!aqz::method_valid(method)) {
+            aqz::set_last_error("Invalid downsampling method: " + std::to_string(method));
+            return AQZ_INVALID_ARGUMENT;
+        }
+        uint32_t unit = 0;
+        std::vector<uint32_t> per_unit(n_levels, 0);
+        if (levels && n_levels > 0 && n_levels <= AQZ_MAX_LEVELS)
+            if (int rc = aqz_shard_unit(levels, n_levels, &unit, per_unit.data()))
+                return rc;
+        auto* n = new aqz_node();
+        for (uint32_t d = 0; d < n_devices; ++d) {
+            aqz_ds* h = nullptr;
+            // aqz_ds_create validates levels, dtype, method and the ordinal
+            if (int rc = aqz_ds_create(levels, n_levels, dtype, method, devices[d], &h)) {
+                aqz_node_destroy(n);
+                return rc;
+            }
+            n->ds.push_back(h);
+        }
+        n->lv.assign(levels, levels + n_levels);
+        for (uint32_t L = 0; L < n_levels; ++L)
+            n->bytes.push_back(aqz_ds_level_bytes(n->ds[0], L));
+        n->unit = unit;
+        n->per_unit = per_unit;
+        *out = n;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(nullptr);
+    }
+}
+
+void
+aqz_node_destroy(aqz_node* n)
+{
+    if (!n)
+        return;
+    for (aqz_ds* h : n->ds)
+        aqz_ds_destroy(h);
+    delete n;
+}
+
+uint32_t
+aqz_node_handle_count(const aqz_node* n)
+{
+    return n ? uint32_t(n->ds.size()) : 0;
+}
+
+aqz_ds*
+aqz_node_handle(aqz_node* n, uint32_t i)
+{
+    return n && i < n->ds.size() ? n->ds[i] : nullptr;
+}
+
+int
+aqz_node_run_host_batch(aqz_node* n,
+                        const void* host_frames,
+                        uint32_t n_frames,
+                        void* const* host_out_levels,
+                        uint32_t* out_counts)
+{
+    try {
+        if (!n)
+            return AQZ_INVALID_ARGUMENT;
+        const uint32_t nl = uint32_t(n->lv.size());
+        if (!host_frames || !host_out_levels)
+            return fail(n, AQZ_INVALID_ARGUMENT, "node_run_host_batch: null buffer");
+        for (uint32_t L = 1; L < nl; ++L)
+            if (!host_out_levels[L])
+                return fail(n, AQZ_INVALID_ARGUMENT,
+                            "node_run_host_batch: null output for level " + std::to_string(L));
+        if (n_frames % n->unit != 0)
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_run_host_batch: " + std::to_string(n_frames) +
+                          " frames is not a whole number of shard units of " +
+                          std::to_string(n->unit) + " (Z pairs must stay on one GPU)");
+        // contiguous blocks of whole units, the first (units % D) handles one
+        // unit more
+        const uint32_t units = n_frames / n->unit;
+        const uint32_t D = uint32_t(n->ds.size());
+        std::vector<uint32_t> first(D + 1, 0);
+        for (uint32_t d = 0; d < D; ++d)
+            first[d + 1] = first[d] + units / D + (d < units % D ? 1 : 0);
+        std::vector<int> rc(D, AQZ_OK);
+        std::vector<std::vector<uint32_t>> counts(D, std::vector<uint32_t>(nl, 0));
+        std::vector<std::thread> workers;
+        auto run = [&](uint32_t d) {
+            const uint32_t u0 = first[d], nu = first[d + 1] - first[d];
+            if (nu == 0)
+                return;
+            std::vector<void*> outs(nl, nullptr);
+            for (uint32_t L = 1; L < nl; ++L)
+                outs[L] = static_cast<uint8_t*>(host_out_levels[L]) +
+                          size_t(u0) * n->per_unit[L] * n->bytes[L];
+            rc[d] = aqz_ds_run_host_batch(
+              n->ds[d],
+              static_cast<const uint8_t*>(host_frames) + size_t(u0) * n->unit * n->bytes[0],
+              nu * n->unit, outs.data(), counts[d].data());
+        };
+        for (uint32_t d = 1; d < D; ++d)
+            workers.emplace_back(run, d);
+        run(0);
+        for (auto& t : workers)
+            t.join();
+        for (uint32_t d = 0; d < D; ++d)
+            if (rc[d])
+                return fail(n, rc[d], "node_run_host_batch: handle " + std::to_string(d) +
+                                        ": " + aqz_ds_last_error(n->ds[d]));
+        for (uint32_t d = 0; d < D; ++d)
+            for (uint32_t L = 1; L < nl; ++L)
+                if (counts[d][L] != (first[d + 1] - first[d]) * n->per_unit[L])
+                    return fail(n, AQZ_INTERNAL_ERROR,
+                                "node_run_host_batch: handle " + std::to_string(d) +
+                                  " emitted an unexpected frame count at level " +
+                                  std::to_string(L));
+        if (out_counts) {
+            out_counts[0] = n_frames;
+            for (uint32_t L = 1; L < nl; ++L)
+                out_counts[L] = units * n->per_unit[L];
+        }
+        n->frames += n_frames;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+const char*
+aqz_node_last_error(const aqz_node* n)
+{
+    return n ? n->err.c_str() : "";
+}
+
+} // extern "C"

@@ -1295,6 +1295,18 @@ aqz_ds_add_frame_async_take(aqz_ds* ds,
             if (t.mode == AQZ_TAKE_HOLD && ds->cached[L] >= 0)
                 return ds->fail_arg("add_frame_async_take: level " + std::to_string(L) +
                                     " is held by the caller but also cached here");
+            // every take buffer is checked before the job is queued, so the
+            // background takes cannot fail half way and leave a level taken
+            // (uncached here) that the caller never learns about
+            if (t.mode == AQZ_TAKE_INTO) {
+                const size_t need = t.tile_rows
+                                      ? tile_geom(ds, L, t.tile_rows, t.tile_cols).tile_bytes
+                                      : ds->bytes[L];
+                if (!t.dst || t.cap < need)
+                    return ds->fail_arg("add_frame_async_take: level " + std::to_string(L) +
+                                        ": take buffer missing or smaller than " +
+                                        std::to_string(need) + " bytes");
+            }
         }
         for (uint32_t L = 1; L < ds->n; ++L)
             ds->held[L] = takes[L].mode == AQZ_TAKE_HOLD;
@@ -1915,19 +1927,35 @@ run_tiled(aqz_ds* ds,
                 (void)hipEventRecord(ds->lattice_done[half], stream);
         }
     } lattice_guard{ ds, half, stream };
-    // A previous batch may still be reading or writing d_chain on another
-    // stream: order this one behind it.
-    if (ds->chain_done)
-        HIP_TRY(ds, hipStreamWaitEvent(stream, ds->chain_done, 0), "hipStreamWaitEvent chain");
-    else
-        HIP_TRY(ds, hipEventCreateWithFlags(&ds->chain_done, hipEventDisableTiming), "event");
-
     // Runs of up to kMaxFusedLevels levels; a run that feeds another also
     // writes its last level row-major into one half of d_chain (the runs
     // alternate halves, so a run never reads the half it writes).  The
     // first chained level is the largest: 1/256 of the base after 4 levels.
     const uint32_t first_feed = aqz::kMaxFusedLevels;
-    if (first_feed + 1 < ds->n) {
+    const bool chained = first_feed + 1 < ds->n;
+    // A previous batch may still be reading or writing d_chain on another
+    // stream: order this one behind it.  Only pyramids deeper than one fused
+    // run touch d_chain, so only they wait and record.  Once the wait is
+    // queued, chain_done is recorded on every way out (ChainGuard), so a
+    // failure after some runs were queued still fences them.
+    if (chained) {
+        if (ds->chain_done)
+            HIP_TRY(ds, hipStreamWaitEvent(stream, ds->chain_done, 0), "hipStreamWaitEvent chain");
+        else
+            HIP_TRY(ds, hipEventCreateWithFlags(&ds->chain_done, hipEventDisableTiming), "event");
+    }
+    struct ChainGuard
+    {
+        aqz_ds* ds;
+        hipStream_t stream;
+        bool on;
+        ~ChainGuard()
+        {
+            if (on)
+                (void)hipEventRecord(ds->chain_done, stream);
+        }
+    } chain_guard{ ds, stream, chained };
+    if (chained) {
         const size_t chain_half = size_t(n_frames) * ds->bytes[first_feed];
         if (ds->d_chain_bytes < 2 * chain_half) {
             HIP_TRY(ds, hipStreamSynchronize(stream), "hipStreamSynchronize");
@@ -1972,7 +2000,6 @@ run_tiled(aqz_ds* ds,
         src = chain;
         L += k;
     }
-    HIP_TRY(ds, hipEventRecord(ds->chain_done, stream), "hipEventRecord chain");
     for (uint32_t l = 0; l < ds->n; ++l) {
         ds->count[l] += n_frames;
         if (out_counts)

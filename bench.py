@@ -13,9 +13,9 @@ barrier and the max-over-ranks of the timed region use torch.distributed.
 
 Rank 0 prints ONE JSON line.  Besides the contract fields it carries
 `roofline` (algorithmic bytes / average kernel duration from HIP events on the
-launch stream, against the 8 TB/s HBM peak), `cpu_baseline` (the C oracle —
-a single-thread port of the reference algorithm — on a bounded sample on this
-host), and `e2e` (host frame -> pinned H2D -> kernels -> D2H -> take_frame
+launch stream, against the 8 TB/s HBM peak), `cpu_baseline` (the reference's
+own downsampler.cpp, compiled unmodified into oracle/_ref, on one core over a
+bounded sample on this host, with the oracle port timed beside it), and `e2e` (host frame -> pinned H2D -> kernels -> D2H -> take_frame
 through the streaming API, the path's real end-to-end rate).
 """
 from __future__ import annotations
@@ -502,16 +502,20 @@ def main():
         if args.cpu_seconds > 0:
             nf = min(B, 8)
             frames = d_in[:nf * frame_bytes].cpu().numpy().view(dtype).reshape(nf, H, W)
-            cpu_baseline = measure_cpu(geo, dtype, method, args.cpu_seconds, list(frames))
+            cpu_baseline = measure_cpu(dims, geo, dtype, method, args.cpu_seconds,
+                                       list(frames))
             threads = min(16, os.cpu_count() or 1)  # the box's CPU share is 16
             if threads > 1:
                 cpu_baseline["parallel"] = measure_cpu_parallel(
-                    geo, dtype, method, max(2.0, args.cpu_seconds / 2), list(frames), threads)
+                    dims, geo, dtype, method, max(2.0, args.cpu_seconds / 2), list(frames), threads)
         if args.e2e_frames > 0:
             e2e = measure_e2e(aqz, geo, dtype, method, args.e2e_frames, device,
                               tile=(chunk, chunk))
             e2e["pipelined"] = measure_e2e_pipelined(aqz, torch, geo, dtype, method,
                                                      d_in, min(B, 64), device)
+            n_vis = torch.cuda.device_count()
+            e2e["node"] = measure_e2e_node(aqz, torch, geo, dtype, method, d_in, min(B, 64),
+                                           list(range(n_vis)) if n_vis > 1 else [device, device])
             e2e["secondary_kernels"] = measure_secondary(aqz, torch, stream, d_in, W, H,
                                                          dtype, chunk)
             # §8(f) row 3 end to end: c-blosc frames of device chunks vs c-blosc
@@ -862,67 +866,109 @@ def host_info():
     return {"cpu_model": model, "nproc": nproc, "os_cpu_count": os.cpu_count()}
 
 
-def measure_cpu(geo, dtype, method, seconds, frames):
-    """The oracle (single-thread C port of the reference Downsampler) on a
-    bounded sample of the same workload: add_frame + take_frame of every
-    level, frame after frame (planes in Z order for volumes), until
-    `seconds` have passed."""
-    import oracle as orc_mod  # cpu_baseline leg: the only non-test user
-    W, H, _ = geo[0]
-    ref = orc_mod.OracleDownsampler(geo, dtype, method)
+def _cpu_impl(dims, geo, dtype, method):
+    """One CPU Downsampler and its per-frame step: the REFERENCE ITSELF
+    (oracle/_ref: downsampler.cpp compiled unmodified with its Release flags,
+    -O3 -mavx2) where it was built, else the oracle port.  Returns
+    (kind, load(frame), step(), what)."""
+    import ref as ref_mod  # cpu_baseline leg: the reference, as the baseline
     n_levels = len(geo)
+    if ref_mod.available():
+        r = ref_mod.RefDownsampler(dims, dtype, method)
+        assert r.geometry == [tuple(g) for g in geo], (r.geometry, geo)
+        take = ref_mod.lib().ref_ds_take_frame
 
-    def one(i):
-        ref.add_frame(frames[i % len(frames)])
-        for L in range(1, n_levels):
-            ref.take_frame(L)
+        def step():
+            # add_frame, then take_frame of every level by swap, as
+            # MultiscaleArray::write_multiscale_frames_ does (no copy out)
+            r.add_buffered()
+            for L in range(1, n_levels):
+                take(r._h, L, None, 0, None)
+        return ("reference", r.load_frame, step,
+                "the reference's own zarr::Downsampler (oracle/_ref: acquire-zarr "
+                "src/streaming/downsampler.cpp compiled unmodified, -O3 -DNDEBUG -mavx2) "
+                "add_frame + take_frame of every level")
+    return _port_impl(geo, dtype, method)  # where oracle/_ref was not built
 
+
+def _time_cpu(kind_pref, dims, geo, dtype, method, seconds, frames):
+    impl = _port_impl(geo, dtype, method) if kind_pref == "port" else \
+        _cpu_impl(dims, geo, dtype, method)
+    kind, load, step, what = impl
     for i in range(2):
-        one(i)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        one(n)
+        load(frames[i % len(frames)])
+        step()
+    n, el = 0, 0.0
+    while el < seconds or n < 4:
+        load(frames[n % len(frames)])   # outside the timed region
+        t0 = time.perf_counter()
+        step()
+        el += time.perf_counter() - t0
         n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 4:
-            break
-    return {"value": round(n * W * H / el / 1e9, 4), "unit": "GPixels/s", "cores": 1,
-            "kind": "port", **host_info(),
-            "sample": f"{n} frames of {W}x{H} {np.dtype(dtype).name} through the "
-                      f"{n_levels}-level pyramid ({el:.1f} s): oracle/ds_oracle.c "
-                      f"Downsampler add_frame+take_frame, single thread (-O3 -mavx2)",
-            "ms_per_frame": round(el / n * 1e3, 3)}
+    return kind, what, n, el
 
 
-def measure_cpu_parallel(geo, dtype, method, seconds, frames, threads):
-    """Upper-bound CPU figure: `threads` host threads, each driving its own
-    oracle Downsampler over its own frames (independent streams, sharded
-    like the GPUs shard frames).  ctypes releases the GIL inside the C calls,
-    so the threads run the C oracle concurrently.  The reference itself runs
-    one downsampler per stream on one consumer thread
-    (zarr.stream.cpp:1616-1630); this is what a host with `threads` free
-    cores could do with as many streams."""
-    import threading
-    import oracle as orc_mod  # cpu_baseline leg only
+def _port_impl(geo, dtype, method):
+    import oracle as orc_mod  # cpu_baseline leg: the port, for the ratio
+    o = orc_mod.OracleDownsampler(geo, dtype, method)
+    cur = {}
+
+    def step():
+        o.add_frame(cur["f"])
+        for L in range(1, len(geo)):
+            o.take_frame(L)
+    return ("port", lambda f: cur.__setitem__("f", f), step,
+            "oracle/ds_oracle.c Downsampler add_frame+take_frame (-O3 -mavx2)")
+
+
+def measure_cpu(dims, geo, dtype, method, seconds, frames):
+    """The CPU baseline on one core over a bounded sample of the same
+    workload: frame after frame (planes in Z order for volumes) until
+    `seconds` of CPU work have been timed.  The reference itself
+    (kind "reference") where oracle/_ref was built; the oracle port is timed
+    beside it for SURVEY §8(d)'s port-vs-reference ratio."""
     W, H, _ = geo[0]
-    n_levels = len(geo)
+    kind, what, n, el = _time_cpu("ref", dims, geo, dtype, method, seconds, frames)
+    out = {"value": round(n * W * H / el / 1e9, 4), "unit": "GPixels/s", "cores": 1,
+           "kind": kind, **host_info(),
+           "sample": f"{n} frames of {W}x{H} {np.dtype(dtype).name} through the "
+                     f"{len(geo)}-level pyramid ({el:.1f} s timed): {what}, single thread",
+           "ms_per_frame": round(el / n * 1e3, 3)}
+    if kind == "reference":
+        _, pwhat, pn, pel = _time_cpu("port", dims, geo, dtype, method,
+                                      max(2.0, seconds / 3), frames)
+        out["port"] = {"value": round(pn * W * H / pel / 1e9, 4),
+                       "ms_per_frame": round(pel / pn * 1e3, 3),
+                       "sample": f"{pn} frames ({pel:.1f} s timed): {pwhat}"}
+        out["reference_over_port_time"] = round((el / n) / (pel / pn), 3)
+    return out
+
+
+def measure_cpu_parallel(dims, geo, dtype, method, seconds, frames, threads):
+    """Upper-bound CPU figure: `threads` host threads, each driving its own
+    Downsampler (the reference where built, else the port) over its own
+    frames (independent streams, sharded like the GPUs shard frames).
+    ctypes releases the GIL inside the C calls, so the threads run
+    concurrently.  The reference itself runs one downsampler per stream on
+    one consumer thread (zarr.stream.cpp:1616-1630); this is what a host with
+    `threads` free cores could do with as many streams."""
+    import threading
+    W, H, _ = geo[0]
     counts = [0] * threads
     start = threading.Barrier(threads + 1, timeout=120)  # a failed worker breaks it
     stop = threading.Event()
+    kinds = [None] * threads
 
     def worker(k):
-        ref = orc_mod.OracleDownsampler(geo, dtype, method)
+        kind, load, step, _ = _cpu_impl(dims, geo, dtype, method)
+        kinds[k] = kind
+        load(frames[k % len(frames)])
         for i in range(2):  # warm
-            ref.add_frame(frames[(k + i) % len(frames)])
-            for L in range(1, n_levels):
-                ref.take_frame(L)
+            step()
         start.wait()
         n = 0
         while not stop.is_set():
-            ref.add_frame(frames[(k + n) % len(frames)])
-            for L in range(1, n_levels):
-                ref.take_frame(L)
+            step()
             n += 1
         counts[k] = n
 
@@ -938,9 +984,9 @@ def measure_cpu_parallel(geo, dtype, method, seconds, frames, threads):
     el = time.perf_counter() - t0
     n = sum(counts)
     return {"value": round(n * W * H / el / 1e9, 4), "unit": "GPixels/s", "cores": threads,
-            "kind": "port",
+            "kind": kinds[0],
             "sample": f"{n} frames of {W}x{H} {np.dtype(dtype).name} over {threads} "
-                      f"threads, one oracle Downsampler each ({el:.1f} s)"}
+                      f"threads, one Downsampler each ({el:.1f} s)"}
 
 
 def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
@@ -1165,6 +1211,39 @@ def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device, dist=
             "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 1),
             "path": "aqz_ds_run_host_batch, pinned host in/out, "
                     f"{n} frames, H2D/kernels/D2H overlapped"}
+
+
+def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
+    """Host-resident frames sharded over `devices` by the library itself
+    (aqz_node_run_host_batch): one handle per entry, each
+    running the pipelined host batch on its block of whole shard units in its
+    own host thread, levels written back in frame-id order.  On a one-GPU box
+    the entries repeat ordinal 0 (two pipelines sharing one PCIe link), so
+    the rate shows the dealing's overhead, not a multi-GPU speed-up."""
+    W, H, _ = geo[0]
+    bpp = np.dtype(dtype).itemsize
+    node = aqz.Node(geo, dtype, method, devices)
+    n -= n % node.unit
+    src = d_in[:n * W * H * bpp].cpu().pin_memory()
+    outs = [None] + [torch.empty(n * w * h * bpp, dtype=torch.uint8).pin_memory()
+                     for w, h, _ in geo[1:]]
+    ptrs = [0] + [o.data_ptr() for o in outs[1:]]
+    node.run_host_batch(src.data_ptr(), n, ptrs)  # warm: allocates the pipelines
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        node.run_host_batch(src.data_ptr(), n, ptrs)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    node.close()
+    in_bytes = n * W * H * bpp
+    out_bytes = sum(o.numel() for o in outs[1:])
+    return {"value": round(n * W * H / best / 1e9, 3), "unit": "GPixels/s",
+            "ms_per_frame": round(best / n * 1e3, 3),
+            "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 1),
+            "devices": list(devices), "shard_unit": node.unit,
+            "path": f"aqz_node_run_host_batch over handles on devices {list(devices)}, "
+                    f"pinned host in/out, {n} frames in blocks of whole shard units"}
 
 
 if __name__ == "__main__":

@@ -191,6 +191,8 @@ int aqz_ds_wait(aqz_ds* ds);
  *     one — chunk-tiled into `dst` like aqz_ds_take_frame_tiled when
  *     tile_rows/tile_cols are nonzero (`tile_nonzero` optional), row-major
  *     like aqz_ds_take_frame when both are 0 — and report has_frame/nbytes;
+ *     `dst` must hold the level's whole (tiled) frame, checked before the job
+ *     is queued (AQZ_INVALID_ARGUMENT otherwise, nothing queued);
  *   AQZ_TAKE_HOLD: the caller still holds an untaken frame of this level
  *     from an earlier INTO take, so this add's frame at the level is dropped,
  *     as Downsampler::emplace_downsampled_frame_ drops a frame while one is
@@ -563,6 +565,68 @@ const char* aqz_method_metadata_json(int method);
 
 /* Library version string. */
 const char* aqz_version(void);
+
+/* ---- Frame sharding over a node's GPUs --------------------
+ *
+ * Frames of a 2-D pyramid are independent, and so are slabs of a volume that
+ * start where add_frame's Z-pairing state is fresh.  An aqz_node deals a host
+ * batch over one aqz_ds handle per device entry — contiguous blocks of whole
+ * shard units, each handle running aqz_ds_run_host_batch on its own streams
+ * and PCIe link in its own host thread — and every block writes its levels at
+ * its frames' place in the outputs, so the caller receives each level in
+ * frame-id order, as `Array::write_frame` requires (array.cpp:179-189).  No
+ * collective: nothing is exchanged between GPUs.
+ */
+
+/*
+ * The shard unit of a pyramid: the fewest level-0 frames (planes) after which
+ * add_frame's state (downsampler.cpp:306-401: stored Z planes and the
+ * odd-stack pass-through count) is back at a fresh handle's.  1 when no level
+ * halves Z; 2^h when h levels halve Z and the planes divide by 2^h; else the
+ * whole stack.  `frames_per_unit` (optional, n_levels entries) receives the
+ * frames each level emits per unit.  Host-only (no device call).
+ */
+int aqz_shard_unit(const aqz_level_desc* levels,
+                   uint32_t n_levels,
+                   uint32_t* unit,
+                   uint32_t* frames_per_unit);
+
+typedef struct aqz_node aqz_node;
+
+/*
+ * One aqz_ds handle per entry of `devices` (HIP ordinals; an ordinal may
+ * repeat, giving several handles on one GPU).  Validation as aqz_ds_create.
+ */
+int aqz_node_create(const aqz_level_desc* levels,
+                    uint32_t n_levels,
+                    int dtype,
+                    int method,
+                    const int* devices,
+                    uint32_t n_devices,
+                    aqz_node** out);
+
+void aqz_node_destroy(aqz_node* node);
+
+/* Number of handles, and handle `i` (NULL when out of range): per-device
+ * diagnostics (aqz_ds_device, aqz_ds_device_memory_usage). */
+uint32_t aqz_node_handle_count(const aqz_node* node);
+aqz_ds* aqz_node_handle(aqz_node* node, uint32_t i);
+
+/*
+ * aqz_ds_run_host_batch over the node: same results, layout and counts as one
+ * handle running the whole batch, with `n_frames` a whole number of shard
+ * units (else AQZ_INVALID_ARGUMENT before anything runs).  Blocks until every
+ * handle has finished; a failing handle's status and message are returned
+ * after all handles have drained.
+ */
+int aqz_node_run_host_batch(aqz_node* node,
+                            const void* host_frames,
+                            uint32_t n_frames,
+                            void* const* host_out_levels,
+                            uint32_t* out_counts);
+
+/* Last error message of the node (never NULL; "" when none). */
+const char* aqz_node_last_error(const aqz_node* node);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,89 @@
+"""GPU: frame sharding inside the library (aqz_node; VERDICT r3
+item 3).  Several handles on ONE GPU (devices [0, 0] and [0, 0, 0]) stand in
+for a node's GPUs: the dealing, the per-handle threads and pipelines and the
+in-order write-back are the same code an 8-GPU node runs.  Every level must
+equal one oracle stream frame for frame — 2-D and volumes, ragged blocks
+(units that do not divide evenly over the handles), batches in a row."""
+import numpy as np
+import pytest
+
+from gpu_util import assert_parity, random_frames
+
+pytestmark = pytest.mark.gpu
+
+SPACE, TIME = 0, 2
+
+CASES = {
+    # name: (dims, frames per batch, batches)
+    "2d_1000x600": ([(TIME, 0, 1, 1), (SPACE, 600, 64, 1), (SPACE, 1000, 64, 1)], 7, 2),
+    "2d_4096_u16": ([(TIME, 0, 1, 1), (SPACE, 4096, 256, 1), (SPACE, 4096, 256, 1)], 5, 1),
+    "vol_z16": ([(TIME, 0, 1, 1), (SPACE, 16, 4, 1), (SPACE, 256, 64, 1), (SPACE, 200, 64, 1)],
+                40, 2),
+    "vol_z15_odd": ([(TIME, 0, 1, 1), (SPACE, 15, 4, 1), (SPACE, 130, 32, 1),
+                     (SPACE, 99, 32, 1)], 45, 1),
+}
+
+
+def _host(nbytes):
+    return np.empty(max(nbytes, 1), np.uint8)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["x2", "x3"])
+@pytest.mark.parametrize("dtype", [np.uint16, np.float32, np.uint8], ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("name", list(CASES))
+def test_node_host_batch_matches_oracle(aqz, oracle, name, dtype, devices):
+    dims, per_batch, batches = CASES[name]
+    if name == "2d_4096_u16" and dtype != np.uint16:
+        pytest.skip("headline geometry: u16")
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    method = aqz.MEAN if dtype != np.uint8 else aqz.MAX
+    node = aqz.Node(geo, dtype, method, devices)
+    assert node.handle_devices() == devices
+    w, h, _ = geo[0]
+    bpp = np.dtype(dtype).itemsize
+    rng = np.random.default_rng(per_batch * 31 + len(devices))
+    ref = oracle.OracleDownsampler(geo, dtype, method)
+    assert per_batch % node.unit == 0
+    try:
+        for b in range(batches):
+            frames = random_frames(rng, dtype, (per_batch, h, w))
+            outs = [None] + [_host(per_batch * gw * gh * bpp) for gw, gh, _ in geo[1:]]
+            counts = node.run_host_batch(frames.ctypes.data, per_batch,
+                                         [0] + [o.ctypes.data for o in outs[1:]])
+            want = {L: [] for L in range(1, len(geo))}
+            for f in frames:
+                ref.add_frame(f)
+                for L in want:
+                    r = ref.take_frame(L)
+                    if r is not None:
+                        want[L].append(r)
+            for L, wl in want.items():
+                gw, gh, _ = geo[L]
+                assert counts[L] == len(wl), f"batch {b} level {L}"
+                got = outs[L][:len(wl) * gw * gh * bpp].view(dtype).reshape(len(wl), gh, gw)
+                for k, e in enumerate(wl):
+                    assert_parity(got[k], e, f"{name} batch {b} L{L} frame {k}")
+    finally:
+        node.close()
+
+
+def test_node_rejects_partial_units(aqz):
+    dims = CASES["vol_z16"][0]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    node = aqz.Node(geo, np.uint16, aqz.MEAN, [0, 0])
+    try:
+        assert node.unit == 4
+        w, h, _ = geo[0]
+        frames = np.zeros((6, h, w), np.uint16)
+        outs = [0] + [_host(6 * gw * gh * 2).ctypes.data for gw, gh, _ in geo[1:]]
+        with pytest.raises(aqz.AqzError) as e:
+            node.run_host_batch(frames.ctypes.data, 6, outs)
+        assert "shard units of 4" in str(e.value)
+    finally:
+        node.close()
+
+
+def test_node_rejects_bad_ordinal(aqz):
+    geo = [(64, 64, 0), (32, 32, 0)]
+    with pytest.raises(aqz.AqzError):
+        aqz.Node(geo, np.uint16, aqz.MEAN, [0, 4096])
