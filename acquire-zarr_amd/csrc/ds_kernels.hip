@@ -437,6 +437,19 @@ int_env(const char* name, int dflt)
     return (e && *e) ? std::atoi(e) : dflt;
 }
 
+// $AQZ_SPLIT_LOADS: 1 / 0 = band kernels of 4- and 8-byte types load each
+// row's 2 KiB wave segment as two contiguous halves (cascade_unit SPLIT) or
+// as 32 bytes per lane; unset: the launcher's default.
+inline bool
+split_loads()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("AQZ_SPLIT_LOADS");
+        return (e && *e) ? std::atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
 // $AQZ_XCD_REMAP: unset = the launcher's default, 0 = off, 1 = on (A/B only).
 inline int
 xcd_remap_env()
@@ -943,8 +956,18 @@ cascade_level(const CascadeParams& p,
 // loads / stores.  Every byte of the pyramid is touched exactly once, so both
 // streams are marked non-temporal: measured on MI355X (tools/microbench.hip,
 // profiles/r01) the headline batch drops from ~530 to ~475 us with NT stores.
+//
+// SPLIT (two 16-byte loads per lane and row, i.e. 4- and 8-byte types at the
+// wide tile): the wave's 64 x 32-byte row segment is loaded as two halves of
+// 64 x 16 contiguous bytes — load k covers bytes [k KiB, (k+1) KiB) of the
+// segment, lane i bytes 16i.. of it — instead of lane i taking bytes 32i..
+// in both loads.  Each load instruction then reads whole 128-byte lines, and
+// no line is requested by two instructions, which L2 did not always merge
+// (F config Min/Max fetched 2.3-2.7% more than the frame).
+// The halves are two tiles of E columns per lane, reduced and stored
+// (staged) one after the other by the E-column cascade.
 template<typename T, int M, int NL, int C, bool NT, bool EDGE, bool NTS = true,
-         int STAGED = 0, int TILED = 0>
+         int STAGED = 0, int TILED = 0, bool SPLIT = false>
 __device__ __forceinline__ void
 cascade_unit(const CascadeParams& p,
              uint32_t f,
@@ -960,6 +983,28 @@ cascade_unit(const CascadeParams& p,
     constexpr int E = LB / int(sizeof(T));   // elements per load
     const T* src =
       reinterpret_cast<const T*>(p.src) + uint64_t(f) * p.src_frame_elems;
+    if constexpr (SPLIT) {
+        static_assert(V == 2 && TILED == 0, "SPLIT: two loads per row, row-major/staged levels");
+        const uint32_t wc0 = col0 - uint32_t(lane) * C; // the wave's first column
+        const bool last_frame = f + 1 == p.total_units / (p.units_x * p.units_y);
+        T h[2][R][E];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                load_chunk<T, E, NT, EDGE>(&h[k][r][0], src + uint64_t(row0 + r) * p.W,
+                                           wc0 + uint32_t(k) * 64u * E + uint32_t(lane) * E, p.W,
+                                           row0 + r < p.H, !last_frame || row0 + r + 1 < p.H);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            cascade_level<T, M, E, 1, NL, R, E, EDGE, NTS, STAGED, TILED>(
+              p, h[k], f, row0, wc0 + uint32_t(k) * 64u * E + uint32_t(lane) * E, lane, sc);
+        }
+        return;
+    }
 
     T v[R][C];
     // All row loads are issued before any arithmetic: 2^NL * V outstanding
@@ -1072,7 +1117,7 @@ cascade_kernel(CascadeParams p)
 // is split into segments of seg_tiles tiles, one workgroup each, every level
 // row of a segment one contiguous piece; waves past the last tile only join
 // the barrier.
-template<typename T, int M, int NL, int C, bool NT = true, bool ROWS = false>
+template<typename T, int M, int NL, int C, bool NT = true, bool ROWS = false, bool SPLIT = false>
 __global__ __launch_bounds__(512)
 // 2-byte Min / Max on line-aligned rows (NT loads): held to 80 VGPRs, 6
 // waves per SIMD instead of 5 at 81 (headline Min 481 -> 470 us, Max 483
@@ -1158,9 +1203,11 @@ cascade_band_kernel(CascadeParams p, uint32_t stage_mask, uint32_t seg_tiles)
         const uint32_t col0 = ux * (64u * C) + uint32_t(lane) * C;
         const bool interior = (ux * 64u * C + 64u * C <= p.W) && (row0 + R <= p.H);
         if (interior)
-            cascade_unit<T, M, NL, C, NT, false, true, ROWS ? 2 : 1>(p, f, row0, col0, lane, &sc);
+            cascade_unit<T, M, NL, C, NT, false, true, ROWS ? 2 : 1, 0, SPLIT>(p, f, row0, col0,
+                                                                           lane, &sc);
         else
-            cascade_unit<T, M, NL, C, NT, true, true, ROWS ? 2 : 1>(p, f, row0, col0, lane, &sc);
+            cascade_unit<T, M, NL, C, NT, true, true, ROWS ? 2 : 1, 0, SPLIT>(p, f, row0, col0,
+                                                                          lane, &sc);
     }
     uint32_t tid = threadIdx.x, nth = blockDim.x;
     if (last_mode) {
@@ -2142,16 +2189,17 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                 constexpr bool NT = decltype(nttag)::value;
                 if (band) {
                     const dim3 blk(64 * band_waves);
-                    auto launch_band = [&](auto rtag) {
+                    auto launch_band = [&](auto rtag, auto stag) {
                         constexpr bool RW = decltype(rtag)::value;
+                        constexpr bool SP = decltype(stag)::value;
                         auto one = [&](auto ltag) {
                             constexpr int NLV = decltype(ltag)::value;
                             if (lds > 65536) // above the default per-workgroup LDS
                                 (void)hipFuncSetAttribute(
                                   reinterpret_cast<const void*>(
-                                    &cascade_band_kernel<T, M, NLV, C, NT, RW>),
+                                    &cascade_band_kernel<T, M, NLV, C, NT, RW, SP>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-                            hipLaunchKernelGGL((cascade_band_kernel<T, M, NLV, C, NT, RW>),
+                            hipLaunchKernelGGL((cascade_band_kernel<T, M, NLV, C, NT, RW, SP>),
                                                dim3(bands), blk, lds, stream, p, stage_mask,
                                                seg_tiles);
                         };
@@ -2168,11 +2216,19 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                     // at the wide tile only (where the launcher picks them)
                     if constexpr ((sizeof(T) == 2 || sizeof(T) == 4) && C == int(CW)) {
                         if (p.seg_rowwise) {
-                            launch_band(std::true_type{});
+                            launch_band(std::true_type{}, std::false_type{});
                             return;
                         }
                     }
-                    launch_band(std::false_type{});
+                    // whole-line loads for 4- and 8-byte types at the wide
+                    // tile (cascade_unit SPLIT); $AQZ_SPLIT_LOADS=0 / 1 (A/B)
+                    if constexpr (sizeof(T) >= 4 && C == int(CW)) {
+                        if (split_loads()) {
+                            launch_band(std::false_type{}, std::true_type{});
+                            return;
+                        }
+                    }
+                    launch_band(std::false_type{}, std::false_type{});
                     return;
                 }
                 switch (n_out) {

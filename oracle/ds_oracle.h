@@ -10,9 +10,11 @@
  * (tests/unit-tests/downsampler.cpp, downsampler-odd-z.cpp) and the pixel
  * expectations of python/tests/test_stream.py, restated as fixtures under
  * tests/golden/; the chunk addressing by the 203 assertions of the
- * reference's tests/unit-tests/array-dimensions-*.cpp.  The reference
- * downsampler is not used as an oracle (downsampler.hh includes
- * nlohmann/json.hpp, absent from this image), see DESIGN.md §3.
+ * reference's tests/unit-tests/array-dimensions-*.cpp.  Since round 4 it is
+ * also pinned by the REFERENCE ITSELF: oracle/_ref (downsampler.cpp compiled
+ * unmodified, `make -C oracle ref`) made tests/golden/reference_vectors.* and
+ * reference_digests.json, which this oracle reproduces byte for byte, and is
+ * fuzzed against it live (tests/test_reference_pin.py); see DESIGN.md §3.
  */
 #ifndef DS_ORACLE_H
 #define DS_ORACLE_H

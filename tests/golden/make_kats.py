@@ -24,10 +24,11 @@ computation.  R7-R9 evaluate the level expectations with the tests' own
 formulas (cited per line).  The script needs /root/reference only when it is
 re-run here; the tests read the committed JSON alone.
 
-No fixture was produced by running reference code: the downsampler's header
-includes nlohmann/json.hpp, which this image lacks, and a build against a
-stand-in header is not used as an oracle.  The Python package
-cannot be built either (its pybind11 dependencies are absent).
+No fixture here is produced by running reference code: these are the
+reference tests' own assertions, transcribed.  Fixtures made by running the
+reference itself (oracle/_ref, compiled unmodified against the image's
+nlohmann/json 3.1.1) are tests/golden/make_reference_vectors.py's.  The
+Python package cannot be built (its pybind11 dependencies are absent).
 
 Run: python tests/golden/make_kats.py
 """
