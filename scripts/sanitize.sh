@@ -23,13 +23,13 @@ for k in 0 1 2 3 4 5 6 7; do
       -o "$OUT/ds_kernels_s$k.o" &
   pids+=($!)
 done
-for f in ds_dispatch.cpp ds_runtime.cpp codec_runtime.cpp blosc_frame.cpp; do
+for f in ds_dispatch.cpp ds_runtime.cpp ds_node.cpp codec_runtime.cpp blosc_frame.cpp; do
   $HIPCC $HF $HS -DAQZ_SHARDS=8 -x hip -c "$ROOT/acquire-zarr_amd/csrc/$f" -o "$OUT/${f%.*}.o"
 done
 $HIPCC $HF $HS -c "$ROOT/acquire-zarr_amd/csrc/codec_kernels.hip" -o "$OUT/codec_kernels.o"
 for p in "${pids[@]}"; do wait "$p"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC -fsanitize=address,undefined \
-    "$OUT"/ds_kernels_s?.o "$OUT/ds_dispatch.o" "$OUT/ds_runtime.o" "$OUT/codec_runtime.o" \
+    "$OUT"/ds_kernels_s?.o "$OUT/ds_dispatch.o" "$OUT/ds_runtime.o" "$OUT/ds_node.o" "$OUT/codec_runtime.o" \
     "$OUT/codec_kernels.o" "$OUT/blosc_frame.o" -o "$OUT/libaqz_san.so" \
     -Wl,-rpath,/opt/rocm/lib -ldl -lpthread
 # the driver must use the same (clang) sanitizer runtime as the library

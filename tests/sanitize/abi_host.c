@@ -106,6 +106,28 @@ main(void)
         aqz_blosc_blocksize(5, 2, nb, "blosclz", &bs) != AQZ_INVALID_ARGUMENT)
         return 21;
     free(src);
+    /* node sharding: shard units (host only) and create-time validation */
+    {
+        aqz_level_desc vol[3] = { { 64, 64, 16 }, { 32, 32, 8 }, { 16, 16, 4 } };
+        aqz_level_desc odd[3] = { { 64, 64, 15 }, { 32, 32, 8 }, { 16, 16, 4 } };
+        aqz_level_desc flat[2] = { { 64, 64, 0 }, { 32, 32, 0 } };
+        uint32_t unit = 0, per[3] = { 0 };
+        if (aqz_shard_unit(vol, 3, &unit, per) || unit != 4 || per[1] != 2 || per[2] != 1)
+            return 22;
+        if (aqz_shard_unit(odd, 3, &unit, per) || unit != 15 || per[1] != 8 || per[2] != 4)
+            return 23;
+        if (aqz_shard_unit(flat, 2, &unit, NULL) || unit != 1)
+            return 24;
+        if (aqz_shard_unit(NULL, 3, &unit, per) != AQZ_INVALID_ARGUMENT)
+            return 25;
+        int devs[2] = { 0, 0 };
+        aqz_node* node = NULL;
+        if (aqz_node_create(vol, 3, 10, 1, devs, 2, &node) != AQZ_INVALID_ARGUMENT || node)
+            return 26;
+        if (aqz_node_create(vol, 3, 1, 1, devs, 0, &node) != AQZ_INVALID_ARGUMENT || node)
+            return 27;
+        aqz_node_destroy(NULL);
+    }
     printf("abi_host: ok (%s; %s)\n", aqz_version(), aqz_blosc_codec_info());
     return 0;
 }

@@ -13,7 +13,8 @@ the same box.
 
 --set volume runs the volume kernel's read patterns instead: every row of
 every plane (Mean), and every other row of every other plane (Decimate), for
-square u16 planes 512-4096 wide.
+square u16 planes 512-4096 wide.  --set decimate: 2-D Decimate's every-other-
+row reads against all rows, for 512^2 u8, 2048^2 and 4096^2 u16 frames.
 """
 import argparse
 import ctypes
@@ -44,12 +45,25 @@ def volume_cases():
     return out
 
 
+def decimate_cases():
+    """Decimate's 2-D read pattern (every other row) against all rows, for
+    the 512^2 u8 frames of config C1b (512-B rows: the skipped half of every
+    1 KiB pair of rows is the neighbour of what is read) and the 4096^2 u16
+    headline (8 KiB rows), VERDICT r3 item 5."""
+    out = []
+    for label, rb, h in (("512x512_u8", 512, 512), ("4096x4096_u16", 8192, 4096),
+                         ("2048x2048_u16", 4096, 2048)):
+        out.append((f"{label}_all_rows", rb, rb, h, rb * h))
+        out.append((f"{label}_decimate", rb, 2 * rb, h // 2, rb * h))
+    return out
+
+
 def main(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--gib", type=float, default=2.0)
     p.add_argument("--json", default="")
-    p.add_argument("--set", default="frames", choices=["frames", "volume"],
+    p.add_argument("--set", default="frames", choices=["frames", "volume", "decimate"],
                    help="frames: dense u16 frames of SHAPES; volume: the volume "
                         "kernel's Mean and Decimate read patterns")
     a = p.parse_args(argv)
@@ -65,7 +79,7 @@ def main(argv=None):
     sink = torch.zeros(16, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.Stream()
     out = open(a.json, "w") if a.json else None
-    cases = volume_cases() if a.set == "volume" else frame_cases()
+    cases = {"volume": volume_cases, "decimate": decimate_cases}.get(a.set, frame_cases)()
     for label, row_bytes, pitch, h, fstride in cases:
         frames = max(1, total // fstride)
         units = frames * (-(-h // 16)) * (-(-row_bytes // 1024))
