@@ -375,6 +375,7 @@ struct CascadeParams
     uint32_t nt;                     // launcher's choice of load policy (load_nt)
     uint32_t band_last;              // K > 0: the band's last K waves to finish store it (no barrier)
     uint32_t seg_rowwise;            // 1: band segments of misaligned rows (StageCtx::rowb)
+    uint32_t upw;                    // units per wave (cascade_kernel, columns-fastest order)
 };
 
 // $AQZ_LOAD_NT: 1 / 0 forces the fused cascade's loads with / without the
@@ -1061,44 +1062,51 @@ cascade_kernel(CascadeParams p)
         if (blk < nb8)
             blk = (blk & 7u) * (nb8 >> 3) + (blk >> 3);
     }
-    uint32_t ux, uy, f;
-    if (!TILED && p.seg_w) {
-        // band-aligned workgroups: the waves that share a row's partial
-        // 64-B bursts run on one CU, so the halves meet in its L2
-        const uint32_t segs = (p.units_x + p.seg_w - 1) / p.seg_w;
-        const uint32_t band = blk / segs;
-        ux = (blk - band * segs) * p.seg_w + wave;
-        if (ux >= p.units_x || band >= p.total_units / p.units_x)
+    // p.upw > 1 (columns-fastest order, no band workgroups): each wave takes
+    // that many consecutive units, for launches whose units move only a few
+    // KiB (Decimate of narrow frames reads 2 of 4 rows of 512 B)
+    const uint32_t upw = (!TILED && !p.seg_w && p.order == 0) ? max(p.upw, 1u) : 1u;
+    for (uint32_t it = 0; it < upw; ++it) {
+        uint32_t ux, uy, f;
+        if (!TILED && p.seg_w) {
+            // band-aligned workgroups: the waves that share a row's partial
+            // 64-B bursts run on one CU, so the halves meet in its L2
+            const uint32_t segs = (p.units_x + p.seg_w - 1) / p.seg_w;
+            const uint32_t band = blk / segs;
+            ux = (blk - band * segs) * p.seg_w + wave;
+            if (ux >= p.units_x || band >= p.total_units / p.units_x)
+                return;
+            uy = band % p.units_y;
+            f = band / p.units_y;
+        } else if (const uint32_t u = (blk * (blockDim.x >> 6) + wave) * upw + it;
+                   u >= p.total_units) {
             return;
-        uy = band % p.units_y;
-        f = band / p.units_y;
-    } else if (const uint32_t u = blk * (blockDim.x >> 6) + wave; u >= p.total_units) {
-        return;
-    } else if (TILED || p.order == 0) {
-        ux = u % p.units_x;
-        const uint32_t t = u / p.units_x;
-        uy = t % p.units_y;
-        f = t / p.units_y;
-    } else if (p.order == 1) {
-        const uint32_t nf = p.total_units / (p.units_x * p.units_y);
-        f = u % nf;
-        const uint32_t t = u / nf;
-        ux = t % p.units_x;
-        uy = t / p.units_x;
-    } else {
-        uy = u % p.units_y;
-        const uint32_t t = u / p.units_y;
-        ux = t % p.units_x;
-        f = t / p.units_x;
-    }
-    const uint32_t row0 = uy * R;
-    const uint32_t tile_col0 = ux * (64u * C);
-    const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
-    // wave-uniform: interior tiles take the edge-free path
-    if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
-        cascade_unit<T, M, NL, C, NT, false, true, 0, TILED>(p, f, row0, col0, lane);
-    } else {
-        cascade_unit<T, M, NL, C, NT, true, true, 0, TILED>(p, f, row0, col0, lane);
+        } else if (TILED || p.order == 0) {
+            ux = u % p.units_x;
+            const uint32_t t = u / p.units_x;
+            uy = t % p.units_y;
+            f = t / p.units_y;
+        } else if (p.order == 1) {
+            const uint32_t nf = p.total_units / (p.units_x * p.units_y);
+            f = u % nf;
+            const uint32_t t = u / nf;
+            ux = t % p.units_x;
+            uy = t / p.units_x;
+        } else {
+            uy = u % p.units_y;
+            const uint32_t t = u / p.units_y;
+            ux = t % p.units_x;
+            f = t / p.units_x;
+        }
+        const uint32_t row0 = uy * R;
+        const uint32_t tile_col0 = ux * (64u * C);
+        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+        // wave-uniform: interior tiles take the edge-free path
+        if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
+            cascade_unit<T, M, NL, C, NT, false, true, 0, TILED>(p, f, row0, col0, lane);
+        } else {
+            cascade_unit<T, M, NL, C, NT, true, true, 0, TILED>(p, f, row0, col0, lane);
+        }
     }
 }
 
@@ -2034,7 +2042,25 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // 4 waves per block, one tile per wave per iteration.
         static const uint32_t wpb = uint32_t(std::clamp(int_env("AQZ_CASCADE_WAVES", 4), 1, 8));
         static const uint32_t order = uint32_t(std::clamp(int_env("AQZ_UNIT_ORDER", 0), 0, 2));
-        const uint32_t grid = grid_for(total, wpb, 0);
+        // Units per wave (cascade_kernel's loop): a wave whose unit reads
+        // under 4 KiB takes 2, 4 or 8 consecutive units, so that it moves at
+        // least that much.  512^2 u8 (2 KiB units; Decimate reads half of
+        // each): Decimate 57.8 -> 39.4 us with 4, Mean 61.5 -> 56.9 and Max
+        // 63.9 -> 57.7 with 2 (4 lost against 2); 2048^2 u16 Decimate (4 KiB
+        // units) lost with 2 (69.1 -> 71.7), so it keeps 1; same box, two
+        // rounds (profiles/r04/upw/).  $AQZ_UNITS_PER_WAVE=k forces k.
+        static const int upw_env = int_env("AQZ_UNITS_PER_WAVE", 0);
+        uint32_t upw = 1;
+        if (upw_env > 0) {
+            upw = uint32_t(std::min(upw_env, 16));
+        } else {
+            const uint64_t unit_bytes = (uint64_t(R) * 64u * cols * sizeof(T)) >>
+                                        (method == kDecimate ? 1 : 0);
+            while (upw < 8 && unit_bytes * upw < 4096)
+                upw *= 2;
+        }
+        p.upw = order == 0 ? upw : 1u;
+        const uint32_t grid = grid_for((total + p.upw - 1) / p.upw, wpb, 0);
         p.main_blocks = grid;
         p.order = order;
         p.remap = xcd_remap_env() == 1;
