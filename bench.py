@@ -471,6 +471,7 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
                 "alg_bytes_per_launch": alg_bytes,
+                "alg_read_bytes_per_launch": read_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
                 "min_launch_us": round(min(launch_ms) * 1e3, 2)}
 
