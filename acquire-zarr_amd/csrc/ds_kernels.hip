@@ -1062,13 +1062,33 @@ cascade_kernel(CascadeParams p)
         if (blk < nb8)
             blk = (blk & 7u) * (nb8 >> 3) + (blk >> 3);
     }
+    if constexpr (TILED) {
+        // one unit per wave (the loop below, even run once, cost the tiled
+        // instantiations 40-70% more VGPRs: headline 60 -> 100, half the
+        // occupancy, 3000^2 tiled 539 -> 710 us)
+        const uint32_t u = blk * (blockDim.x >> 6) + wave;
+        if (u >= p.total_units)
+            return;
+        const uint32_t ux = u % p.units_x;
+        const uint32_t t = u / p.units_x;
+        const uint32_t uy = t % p.units_y;
+        const uint32_t f = t / p.units_y;
+        const uint32_t row0 = uy * R;
+        const uint32_t tile_col0 = ux * (64u * C);
+        const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
+        if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H))
+            cascade_unit<T, M, NL, C, NT, false, true, 0, TILED>(p, f, row0, col0, lane);
+        else
+            cascade_unit<T, M, NL, C, NT, true, true, 0, TILED>(p, f, row0, col0, lane);
+        return;
+    }
     // p.upw > 1 (columns-fastest order, no band workgroups): each wave takes
     // that many consecutive units, for launches whose units move only a few
     // KiB (Decimate of narrow frames reads 2 of 4 rows of 512 B)
-    const uint32_t upw = (!TILED && !p.seg_w && p.order == 0) ? max(p.upw, 1u) : 1u;
+    const uint32_t upw = (!p.seg_w && p.order == 0) ? max(p.upw, 1u) : 1u;
     for (uint32_t it = 0; it < upw; ++it) {
         uint32_t ux, uy, f;
-        if (!TILED && p.seg_w) {
+        if (p.seg_w) {
             // band-aligned workgroups: the waves that share a row's partial
             // 64-B bursts run on one CU, so the halves meet in its L2
             const uint32_t segs = (p.units_x + p.seg_w - 1) / p.seg_w;
@@ -1081,7 +1101,7 @@ cascade_kernel(CascadeParams p)
         } else if (const uint32_t u = (blk * (blockDim.x >> 6) + wave) * upw + it;
                    u >= p.total_units) {
             return;
-        } else if (TILED || p.order == 0) {
+        } else if (p.order == 0) {
             ux = u % p.units_x;
             const uint32_t t = u / p.units_x;
             uy = t % p.units_y;
@@ -1103,9 +1123,9 @@ cascade_kernel(CascadeParams p)
         const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
         // wave-uniform: interior tiles take the edge-free path
         if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
-            cascade_unit<T, M, NL, C, NT, false, true, 0, TILED>(p, f, row0, col0, lane);
+            cascade_unit<T, M, NL, C, NT, false, true, 0, 0>(p, f, row0, col0, lane);
         } else {
-            cascade_unit<T, M, NL, C, NT, true, true, 0, TILED>(p, f, row0, col0, lane);
+            cascade_unit<T, M, NL, C, NT, true, true, 0, 0>(p, f, row0, col0, lane);
         }
     }
 }

@@ -246,6 +246,9 @@ def parse(argv=None):
     p.add_argument("--shape", default="",
                    help="WxH: override the workload's frame size (same dtype, chunk "
                         "and batch bytes), e.g. 5472x3648")
+    p.add_argument("--per-launch-events", action="store_true",
+                   help="an event pair around every launch (per-launch min; adds a "
+                        "~12 us gap between kernels)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
@@ -429,16 +432,30 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # per-launch kernel timing with HIP events on the launch stream (in
-    # --xgmi-scatter mode the kernel's own pair sits between the p2p batches)
+    # Kernel timing with HIP events on the launch stream.  Default: one event
+    # before the first launch of the timed region and one after the last, so
+    # the launches run back to back as in production and the average launch
+    # is span / steps — an event pair around every launch left a 12 us gap
+    # between kernels (2.7% at the headline; profiles/r04/bench/).  In
+    # --xgmi-scatter mode (and with --per-launch-events) every launch gets
+    # its own pair, so the kernel's time sits apart from the p2p batches.
+    per_launch = xgmi or args.per_launch_events
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
-           for _ in range(args.steps)]
+           for _ in range(args.steps if per_launch else 1)]
 
     def timed_step(i):
-        step(evs[i])
+        if per_launch:
+            step(evs[i])
+            return
+        if i == 0:
+            evs[0][1].record(stream)
+        step()
+        if i == args.steps - 1:
+            evs[0][2].record(stream)
 
     elapsed = timed_region(timed_step, args.steps, dist, torch.cuda.synchronize)
-    launch_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    launch_ms = ([e[1].elapsed_time(e[2]) for e in evs] if per_launch else
+                 [evs[0][1].elapsed_time(evs[0][2]) / args.steps])
     comm_ms = ([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3]) for e in evs]
                if xgmi else None)
     dev = "cuda" if (dist is not None and dist.get_backend() == "nccl") else "cpu"
@@ -473,7 +490,10 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_read_bytes_per_launch": read_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
-                "min_launch_us": round(min(launch_ms) * 1e3, 2)}
+                "min_launch_us": round(min(launch_ms) * 1e3, 2) if per_launch else None,
+                "launch_timing": ("HIP event pair around every launch" if per_launch else
+                                  f"HIP events around the {args.steps} back-to-back launches "
+                                  "of the timed region, on the launch stream")}
 
     if world > 1:
         # kernel-only fractions: in --xgmi-scatter mode the p2p time is
