@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libaqz_downsampler.so")
+# $AQZ_LIB_PATH: a variant build for A/B measurements (tools/, profiles/);
+# unset, the in-tree library is the one loaded
+LIB_PATH = os.environ.get("AQZ_LIB_PATH") or os.path.join(PKG_DIR, "libaqz_downsampler.so")
 
 # ZarrDataType (zarr.types.h:55-68), ZarrDownsamplingMethod (:90-97),
 # ZarrDimensionType (:81-88) numeric values.
