@@ -51,6 +51,7 @@ EXPORTS = (
     "aqz_method_metadata_json", "aqz_version",
     "aqz_shard_unit", "aqz_node_create", "aqz_node_destroy", "aqz_node_handle_count",
     "aqz_node_handle", "aqz_node_run_host_batch", "aqz_node_last_error",
+    "aqz_node_add_frame", "aqz_node_take_frame", "aqz_node_flush",
 )
 
 
@@ -210,6 +211,9 @@ def lib() -> ctypes.CDLL:
     L.aqz_node_run_host_batch.argtypes = [vp, vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u32)]
     L.aqz_node_last_error.argtypes = [vp]
     L.aqz_node_last_error.restype = ctypes.c_char_p
+    L.aqz_node_add_frame.argtypes = [vp, vp, sz]
+    L.aqz_node_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(i32)]
+    L.aqz_node_flush.argtypes = [vp]
     _lib = L
     return L
 
@@ -744,12 +748,46 @@ class Node:
             raise AqzError(rc, L.aqz_last_error().decode())
         self._h = h
         self.unit, self.frames_per_unit = shard_unit(self.geometry)
+        # frames handed to aqz_node_add_frame stay referenced until their
+        # handle is reused (unit x handles adds later) or flush() returns
+        import collections
+        self._inflight = collections.deque(maxlen=self.unit * len(devices) + 1)
 
     def close(self):
         h = getattr(self, "_h", None)
         if h:
             lib().aqz_node_destroy(h)
             self._h = None
+        if hasattr(self, "_inflight"):
+            self._inflight.clear()
+
+    def _check(self, rc):
+        if rc:
+            raise AqzError(rc, lib().aqz_node_last_error(self._h).decode())
+
+    def add_frame(self, frame: np.ndarray):
+        """aqz_node_add_frame: deal the frame to its handle, return at once."""
+        frame = np.ascontiguousarray(frame)
+        if frame.dtype != self.dtype:
+            raise TypeError(f"frame dtype {frame.dtype} != {self.dtype}")
+        self._check(lib().aqz_node_add_frame(self._h, frame.ctypes.data, frame.nbytes))
+        self._inflight.append(frame)
+
+    def take_frame(self, level: int):
+        """Next level frame in emission order, or None if none is ready."""
+        w, h, _ = self.geometry[level]
+        out = np.empty((h, w), dtype=self.dtype)
+        nb = ctypes.c_size_t(0)
+        has = ctypes.c_int(0)
+        self._check(lib().aqz_node_take_frame(self._h, level, out.ctypes.data, out.nbytes,
+                                              ctypes.byref(nb), ctypes.byref(has)))
+        return out if has.value else None
+
+    def flush(self):
+        try:
+            self._check(lib().aqz_node_flush(self._h))
+        finally:
+            self._inflight.clear()
 
     def __del__(self):
         self.close()

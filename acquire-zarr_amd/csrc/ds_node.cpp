@@ -22,6 +22,12 @@
 //   * otherwise: the whole stack, P planes.
 // aqz_shard_unit checks the unit by running add_frame's control flow
 // (counts only) over one unit from a fresh state.
+//
+// Streaming (aqz_node_add_frame / _take_frame / _flush): frame k goes to
+// handle (k / unit) % D as an add_frame_async that takes every level in its
+// background job, so up to D frames (one per handle) are in flight; levels
+// are queued in submission order and handed out in the order one
+// Downsampler emits them.
 #include "aqz_downsampler.h"
 #include "abi_guard.hh"
 #include "ds_kernels.hh"
@@ -30,6 +36,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <thread>
 #include <vector>
@@ -41,8 +48,23 @@ struct aqz_node
     std::vector<size_t> bytes;      // one frame per level
     uint32_t unit = 1;              // level-0 frames per shard unit
     std::vector<uint32_t> per_unit; // frames each level emits per unit
-    uint64_t frames = 0;            // level-0 frames taken so far
+    uint64_t frames = 0;            // level-0 frames taken so far (batches and stream)
     std::string err;
+
+    // Streaming (aqz_node_add_frame): one add in flight per handle, each
+    // taking every level into node-owned buffers in its background job
+    // (aqz_ds_add_frame_async_take); adds are published in submission order.
+    struct Add
+    {
+        uint32_t handle = 0;
+        bool settled = false;
+        std::vector<aqz_level_take> takes;
+        std::vector<std::vector<uint8_t>> bufs;
+    };
+    std::deque<Add> adds;                             // submission order
+    std::vector<Add*> in_flight;                      // per handle, or null
+    std::vector<std::deque<std::vector<uint8_t>>> ready; // per level, in order
+    std::vector<std::vector<uint8_t>> pool;           // spare take buffers
 };
 
 namespace aqz {
@@ -86,6 +108,55 @@ int
 fail(aqz_node* n, int rc, const std::string& what)
 {
     n->err = what;
+    return rc;
+}
+
+// Wait for handle h's add in flight; its takes become publishable.
+int
+settle_handle(aqz_node* n, uint32_t h)
+{
+    aqz_node::Add* a = n->in_flight[h];
+    if (!a)
+        return AQZ_OK;
+    n->in_flight[h] = nullptr;
+    const int rc = aqz_ds_wait(n->ds[h]);
+    a->settled = true;
+    if (rc)
+        return fail(n, rc, "node add on handle " + std::to_string(h) + ": " +
+                             aqz_ds_last_error(n->ds[h]));
+    return AQZ_OK;
+}
+
+// Move the takes of every settled add at the front of the submission order
+// to the per-level queues: each level's frames come out in the order a
+// single Downsampler would have emitted them.
+void
+publish(aqz_node* n)
+{
+    while (!n->adds.empty() && n->adds.front().settled) {
+        aqz_node::Add& a = n->adds.front();
+        for (size_t L = 1; L < a.takes.size(); ++L) {
+            if (a.takes[L].has_frame)
+                n->ready[L].push_back(std::move(a.bufs[L]));
+            else if (!a.bufs[L].empty())
+                n->pool.push_back(std::move(a.bufs[L]));
+        }
+        n->adds.pop_front();
+    }
+}
+
+int
+flush_all(aqz_node* n)
+{
+    int rc = AQZ_OK;
+    // in submission order, so a failure reports the earliest failed add
+    for (auto& a : n->adds)
+        if (!a.settled && n->in_flight[a.handle] == &a) {
+            const int r = settle_handle(n, a.handle);
+            if (r && !rc)
+                rc = r;
+        }
+    publish(n);
     return rc;
 }
 
@@ -193,6 +264,8 @@ aqz_node_create(const aqz_level_desc* levels,
             n->bytes.push_back(aqz_ds_level_bytes(n->ds[0], L));
         n->unit = unit;
         n->per_unit = per_unit;
+        n->in_flight.assign(n_devices, nullptr);
+        n->ready.resize(n_levels);
         *out = n;
         return AQZ_OK;
     } catch (...) {
@@ -205,9 +278,106 @@ aqz_node_destroy(aqz_node* n)
 {
     if (!n)
         return;
+    // aqz_ds_destroy settles a handle's add in flight before freeing it, so
+    // no background take still writes into this node's buffers
     for (aqz_ds* h : n->ds)
         aqz_ds_destroy(h);
     delete n;
+}
+
+int
+aqz_node_add_frame(aqz_node* n, const void* host_frame, size_t nbytes)
+{
+    try {
+        if (!n)
+            return AQZ_INVALID_ARGUMENT;
+        if (!host_frame || nbytes != n->bytes[0])
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_add_frame: frame of " + std::to_string(nbytes) + " bytes, expected " +
+                          std::to_string(n->bytes[0]));
+        const uint32_t D = uint32_t(n->ds.size());
+        const uint32_t h = uint32_t((n->frames / n->unit) % D);
+        // the handle's previous add (D units ago, or the previous frame of
+        // this unit) must be done before its take buffers are reused
+        if (int rc = settle_handle(n, h))
+            return rc;
+        publish(n);
+        const uint32_t nl = uint32_t(n->lv.size());
+        n->adds.emplace_back();
+        aqz_node::Add& a = n->adds.back();
+        a.handle = h;
+        a.takes.assign(nl, aqz_level_take{});
+        a.bufs.resize(nl);
+        for (uint32_t L = 1; L < nl; ++L) {
+            auto& b = a.bufs[L];
+            if (!n->pool.empty()) {
+                b = std::move(n->pool.back());
+                n->pool.pop_back();
+            }
+            b.resize(n->bytes[L]);
+            a.takes[L].mode = AQZ_TAKE_INTO;
+            a.takes[L].dst = b.data();
+            a.takes[L].cap = b.size();
+        }
+        const int rc = aqz_ds_add_frame_async_take(n->ds[h], host_frame, nbytes, a.takes.data());
+        if (rc) {
+            n->adds.pop_back();
+            return fail(n, rc, std::string("node_add_frame: ") + aqz_ds_last_error(n->ds[h]));
+        }
+        n->in_flight[h] = &a;
+        ++n->frames;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+int
+aqz_node_take_frame(aqz_node* n,
+                    uint32_t level,
+                    void* dst,
+                    size_t cap,
+                    size_t* nbytes,
+                    int* has_frame)
+{
+    try {
+        if (!n || !has_frame)
+            return AQZ_INVALID_ARGUMENT;
+        *has_frame = 0;
+        if (nbytes)
+            *nbytes = 0;
+        if (level == 0 || level >= n->lv.size())
+            return AQZ_OK;
+        publish(n);
+        auto& q = n->ready[level];
+        if (q.empty())
+            return AQZ_OK;
+        if (nbytes)
+            *nbytes = q.front().size();
+        *has_frame = 1;
+        if (!dst)
+            return AQZ_OK; // size query: the frame stays queued
+        if (cap < q.front().size())
+            return fail(n, AQZ_INVALID_ARGUMENT, "node_take_frame: buffer too small");
+        std::memcpy(dst, q.front().data(), q.front().size());
+        n->pool.push_back(std::move(q.front()));
+        q.pop_front();
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+int
+aqz_node_flush(aqz_node* n)
+{
+    try {
+        if (!n)
+            return AQZ_INVALID_ARGUMENT;
+        return flush_all(n);
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
 }
 
 uint32_t
@@ -239,6 +409,13 @@ aqz_node_run_host_batch(aqz_node* n,
             if (!host_out_levels[L])
                 return fail(n, AQZ_INVALID_ARGUMENT,
                             "node_run_host_batch: null output for level " + std::to_string(L));
+        if (n->frames % n->unit != 0)
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_run_host_batch: the stream stands inside a shard unit (" +
+                          std::to_string(n->frames % n->unit) + " of " +
+                          std::to_string(n->unit) + " frames)");
+        if (int rc = flush_all(n))
+            return rc;
         if (n_frames % n->unit != 0)
             return fail(n, AQZ_INVALID_ARGUMENT,
                         "node_run_host_batch: " + std::to_string(n_frames) +

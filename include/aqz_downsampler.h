@@ -615,15 +615,46 @@ aqz_ds* aqz_node_handle(aqz_node* node, uint32_t i);
 /*
  * aqz_ds_run_host_batch over the node: same results, layout and counts as one
  * handle running the whole batch, with `n_frames` a whole number of shard
- * units (else AQZ_INVALID_ARGUMENT before anything runs).  Blocks until every
- * handle has finished; a failing handle's status and message are returned
- * after all handles have drained.
+ * units, starting where the stream (aqz_node_add_frame) stands on a unit
+ * boundary (else AQZ_INVALID_ARGUMENT before anything runs); adds in flight
+ * are flushed first.  Blocks until every handle has finished; a failing
+ * handle's status and message are returned after all handles have drained.
  */
 int aqz_node_run_host_batch(aqz_node* node,
                             const void* host_frames,
                             uint32_t n_frames,
                             void* const* host_out_levels,
                             uint32_t* out_counts);
+
+/*
+ * Streaming over the node: several frames in flight, one per handle.  Frame k
+ * goes to handle (k / unit) % n_handles as an aqz_ds_add_frame_async_take that
+ * takes every level into node-owned buffers; the call returns once the frame
+ * is handed to that handle's upload thread (after settling the handle's
+ * previous add).  `host_frame` must stay valid and unchanged until the handle
+ * is used again (unit x n_handles frames later) or aqz_node_flush returns.
+ * Same frames, in the same per-level order, as one Downsampler fed the stream
+ * with every level taken after every frame (the MultiscaleArray caller,
+ * multiscale.array.cpp:298-325) — the emplace rule never applies, since the
+ * node takes every frame.
+ */
+int aqz_node_add_frame(aqz_node* node, const void* host_frame, size_t nbytes);
+
+/*
+ * The next level-`level` frame in emission order, if its add has completed
+ * (non-blocking: *has_frame = 0 when none is ready yet; aqz_node_flush makes
+ * every frame of the adds so far ready).  `dst` NULL: size query, the frame
+ * stays queued.
+ */
+int aqz_node_take_frame(aqz_node* node,
+                        uint32_t level,
+                        void* dst,
+                        size_t cap,
+                        size_t* nbytes,
+                        int* has_frame);
+
+/* Wait for every add in flight; their level frames become takeable. */
+int aqz_node_flush(aqz_node* node);
 
 /* Last error message of the node (never NULL; "" when none). */
 const char* aqz_node_last_error(const aqz_node* node);

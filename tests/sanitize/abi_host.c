@@ -127,6 +127,11 @@ main(void)
         if (aqz_node_create(vol, 3, 1, 1, devs, 0, &node) != AQZ_INVALID_ARGUMENT || node)
             return 27;
         aqz_node_destroy(NULL);
+        int has = 1;
+        if (aqz_node_add_frame(NULL, devs, 4) != AQZ_INVALID_ARGUMENT ||
+            aqz_node_take_frame(NULL, 1, NULL, 0, NULL, &has) != AQZ_INVALID_ARGUMENT ||
+            aqz_node_flush(NULL) != AQZ_INVALID_ARGUMENT)
+            return 28;
     }
     printf("abi_host: ok (%s; %s)\n", aqz_version(), aqz_blosc_codec_info());
     return 0;

@@ -87,3 +87,105 @@ def test_node_rejects_bad_ordinal(aqz):
     geo = [(64, 64, 0), (32, 32, 0)]
     with pytest.raises(aqz.AqzError):
         aqz.Node(geo, np.uint16, aqz.MEAN, [0, 4096])
+
+
+def _oracle_levels(oracle, geo, dtype, method, frames):
+    ref = oracle.OracleDownsampler(geo, dtype, method)
+    want = {L: [] for L in range(1, len(geo))}
+    for f in frames:
+        ref.add_frame(f)
+        for L in want:
+            r = ref.take_frame(L)
+            if r is not None:
+                want[L].append(r)
+    return want
+
+
+STREAM_CASES = {
+    "2d_1000x600": ([(TIME, 0, 1, 1), (SPACE, 600, 64, 1), (SPACE, 1000, 64, 1)], 11),
+    "vol_z16": ([(TIME, 0, 1, 1), (SPACE, 16, 4, 1), (SPACE, 256, 64, 1), (SPACE, 200, 64, 1)], 40),
+    "vol_z15_odd": ([(TIME, 0, 1, 1), (SPACE, 15, 4, 1), (SPACE, 130, 32, 1),
+                     (SPACE, 99, 32, 1)], 37),   # ends inside a stack
+}
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["x2", "x3"])
+@pytest.mark.parametrize("dtype", [np.uint16, np.float32], ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("name", list(STREAM_CASES))
+def test_node_stream_matches_oracle(aqz, oracle, name, dtype, devices):
+    """aqz_node_add_frame / _take_frame / _flush: frames in flight on every
+    handle, levels taken whenever ready, the rest after the flush — the same
+    frames in the same order as one oracle stream."""
+    dims, n = STREAM_CASES[name]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    node = aqz.Node(geo, dtype, aqz.MEAN, devices)
+    rng = np.random.default_rng(n + len(devices))
+    w, h, _ = geo[0]
+    frames = random_frames(rng, dtype, (n, h, w))
+    got = {L: [] for L in range(1, len(geo))}
+    try:
+        for k in range(n):
+            node.add_frame(frames[k])
+            for L in got:
+                while (r := node.take_frame(L)) is not None:
+                    got[L].append(r)
+        node.flush()
+        for L in got:
+            while (r := node.take_frame(L)) is not None:
+                got[L].append(r)
+    finally:
+        node.close()
+    want = _oracle_levels(oracle, geo, dtype, aqz.MEAN, frames)
+    for L in got:
+        assert len(got[L]) == len(want[L]), f"{name} level {L}: {len(got[L])} vs {len(want[L])}"
+        for k, (a, b) in enumerate(zip(got[L], want[L])):
+            assert_parity(a, b, f"{name} stream L{L} frame {k}")
+
+
+def test_node_stream_then_batch_then_stream(aqz, oracle):
+    """A batch may follow the stream at a shard-unit boundary (the stream's
+    adds are flushed first) and the stream continues after it; inside a unit
+    the batch is refused."""
+    dims = STREAM_CASES["vol_z16"][0]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    node = aqz.Node(geo, np.uint16, aqz.MAX, [0, 0])
+    w, h, _ = geo[0]
+    rng = np.random.default_rng(5)
+    frames = random_frames(rng, np.uint16, (24, h, w))
+    got = {L: [] for L in range(1, len(geo))}
+
+    def drain():
+        for L in got:
+            while (r := node.take_frame(L)) is not None:
+                got[L].append(r)
+    try:
+        for k in range(6):                       # 1.5 units
+            node.add_frame(frames[k])
+        outs = [0] + [_host(8 * gw * gh * 2).ctypes.data for gw, gh, _ in geo[1:]]
+        with pytest.raises(aqz.AqzError) as e:
+            node.run_host_batch(frames[6:].ctypes.data, 8, outs)
+        assert "inside a shard unit" in str(e.value)
+        for k in range(6, 8):                    # back on a unit boundary
+            node.add_frame(frames[k])
+        bufs = [None] + [_host(12 * gw * gh * 2) for gw, gh, _ in geo[1:]]
+        drain_before = None
+        counts = node.run_host_batch(frames[8:20].ctypes.data, 12,
+                                     [0] + [b.ctypes.data for b in bufs[1:]])
+        drain()                                  # the stream's frames, flushed by the batch
+        drain_before = {L: len(v) for L, v in got.items()}
+        for L in got:
+            gw, gh, _ = geo[L]
+            got[L] += list(bufs[L][:counts[L] * gw * gh * 2].view(np.uint16)
+                           .reshape(counts[L], gh, gw))
+        for k in range(20, 24):
+            node.add_frame(frames[k])
+        node.flush()
+        drain()
+    finally:
+        node.close()
+    assert drain_before is not None
+    want = _oracle_levels(oracle, geo, np.uint16, aqz.MAX, frames)
+    for L in got:
+        assert len(got[L]) == len(want[L])
+        for k, (a, b) in enumerate(zip(got[L], want[L])):
+            assert_parity(a, b, f"mixed L{L} frame {k}")
