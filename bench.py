@@ -1256,6 +1256,29 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
         node.run_host_batch(src.data_ptr(), n, ptrs)
         el = time.perf_counter() - t0
         best = el if best is None else min(best, el)
+    # the streaming form: one pageable frame per call, as the frame queue
+    # hands them over, levels taken whenever ready, then flushed
+    host = src.numpy().view(dtype).reshape(n, H, W)
+    frames = [np.array(host[k]) for k in range(min(n, 32))]
+    levels = range(1, len(geo))
+
+    def stream():
+        for f in frames:
+            node.add_frame(f)
+            for L in levels:
+                while node.take_frame(L) is not None:
+                    pass
+        node.flush()
+        for L in levels:
+            while node.take_frame(L) is not None:
+                pass
+    stream()  # warm
+    sbest = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        stream()
+        el = time.perf_counter() - t0
+        sbest = el if sbest is None else min(sbest, el)
     node.close()
     in_bytes = n * W * H * bpp
     out_bytes = sum(o.numel() for o in outs[1:])
@@ -1263,6 +1286,9 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
             "ms_per_frame": round(best / n * 1e3, 3),
             "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 1),
             "devices": list(devices), "shard_unit": node.unit,
+            "stream_ms_per_frame": round(sbest / len(frames) * 1e3, 3),
+            "stream_path": f"aqz_node_add_frame of {len(frames)} pageable frames, every level "
+                           "taken when ready, then aqz_node_flush",
             "path": f"aqz_node_run_host_batch over handles on devices {list(devices)}, "
                     f"pinned host in/out, {n} frames in blocks of whole shard units"}
 
