@@ -2204,6 +2204,12 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             seg_tiles = (p.units_x + nseg - 1) / nseg;
             band_waves = seg_tiles;
             p.seg_rowwise = 1;
+            // these segments are stored by their last two waves: 6000x4000
+            // u16 552-555 -> 540-542 us, 5472x3648 530-537 -> 521-526 (same
+            // box, two rounds, profiles/r04/misseg/); whole misaligned
+            // bands of <= 6 tiles keep one (3000^2 548-550 -> 600 us with two)
+            if (band_last_env < 0)
+                p.band_last = 2;
         }
         const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask,
                                             seg_tiles * 64u * cols, p.seg_rowwise != 0);
