@@ -2204,12 +2204,15 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             seg_tiles = (p.units_x + nseg - 1) / nseg;
             band_waves = seg_tiles;
             p.seg_rowwise = 1;
-            // these segments are stored by their last two waves: 6000x4000
-            // u16 552-555 -> 540-542 us, 5472x3648 530-537 -> 521-526 (same
-            // box, two rounds, profiles/r04/misseg/); whole misaligned
-            // bands of <= 6 tiles keep one (3000^2 548-550 -> 600 us with two)
+            // these segments are stored by their last two waves when level
+            // 1's rows split bursts: u16 6000x4000 556 -> 543 us, 5472x3648
+            // 535 -> 523, 4100^2 597 -> 582, f32 6000x4000 1085 -> 1045,
+            // 4100^2 1074 -> 1060; but f32 5472x3648 (level 1 whole bursts)
+            // 1087 -> 1117, so it keeps one (same box, two rounds,
+            // profiles/r04/misseg/).  Whole misaligned bands of <= 6 tiles
+            // keep one too (3000^2 548-550 -> 600 us with two).
             if (band_last_env < 0)
-                p.band_last = 2;
+                p.band_last = (stage_mask & 1u) ? 2u : 1u;
         }
         const uint32_t lds = band_lds_bytes(sizeof(T), outs, n_out, stage_mask,
                                             seg_tiles * 64u * cols, p.seg_rowwise != 0);

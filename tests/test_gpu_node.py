@@ -4,6 +4,8 @@ for a node's GPUs: the dealing, the per-handle threads and pipelines and the
 in-order write-back are the same code an 8-GPU node runs.  Every level must
 equal one oracle stream frame for frame — 2-D and volumes, ragged blocks
 (units that do not divide evenly over the handles), batches in a row."""
+import zlib
+
 import numpy as np
 import pytest
 
@@ -168,7 +170,6 @@ def test_node_stream_then_batch_then_stream(aqz, oracle):
         for k in range(6, 8):                    # back on a unit boundary
             node.add_frame(frames[k])
         bufs = [None] + [_host(12 * gw * gh * 2) for gw, gh, _ in geo[1:]]
-        drain_before = None
         counts = node.run_host_batch(frames[8:20].ctypes.data, 12,
                                      [0] + [b.ctypes.data for b in bufs[1:]])
         drain()                                  # the stream's frames, flushed by the batch
@@ -189,3 +190,61 @@ def test_node_stream_then_batch_then_stream(aqz, oracle):
         assert len(got[L]) == len(want[L])
         for k, (a, b) in enumerate(zip(got[L], want[L])):
             assert_parity(a, b, f"mixed L{L} frame {k}")
+
+
+def _fuzz_case(i):
+    rng = np.random.default_rng(zlib.crc32(f"nodefuzz{i}".encode()))
+    dtype = [np.uint8, np.uint16, np.int32, np.float32, np.float64][int(rng.integers(5))]
+    method = int(rng.integers(4))
+    w, h = int(rng.integers(8, 700)), int(rng.integers(4, 300))
+    cx, cy = int(rng.integers(8, 128)), int(rng.integers(4, 128))
+    dims = [(TIME, 0, 1, 1)]
+    if rng.random() < 0.5:                      # a Z stack
+        z = int(rng.integers(2, 20))
+        dims.append((SPACE, z, int(rng.integers(1, 6)), 1))
+    dims += [(SPACE, h, cy, 1), (SPACE, w, cx, 1)]
+    devices = [0] * int(rng.integers(1, 5))
+    return dtype, method, dims, devices, rng
+
+
+@pytest.mark.parametrize("i", range(24))
+def test_node_fuzz(aqz, oracle, i):
+    """Random 2-D and Z-stack geometries (even and odd stacks, Z halving at
+    some levels only), dtypes, methods and 1-4 handles: a host batch of whole
+    units, then a stream of any length, against one oracle stream."""
+    dtype, method, dims, devices, rng = _fuzz_case(i)
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    if len(geo) < 2:
+        pytest.skip("no level below the base")
+    node = aqz.Node(geo, dtype, method, devices)
+    w, h, _ = geo[0]
+    n_batch = node.unit * int(rng.integers(1, 5))
+    n_stream = int(rng.integers(1, 2 * node.unit + 3))
+    frames = random_frames(rng, dtype, (n_batch + n_stream, h, w))
+    bpp = np.dtype(dtype).itemsize
+    got = {L: [] for L in range(1, len(geo))}
+    try:
+        bufs = [None] + [_host(n_batch * gw * gh * bpp) for gw, gh, _ in geo[1:]]
+        counts = node.run_host_batch(frames[:n_batch].ctypes.data, n_batch,
+                                     [0] + [b.ctypes.data for b in bufs[1:]])
+        for L in got:
+            gw, gh, _ = geo[L]
+            got[L] += list(bufs[L][:counts[L] * gw * gh * bpp].view(dtype)
+                           .reshape(counts[L], gh, gw))
+        for k in range(n_batch, n_batch + n_stream):
+            node.add_frame(frames[k])
+            if rng.random() < 0.5:
+                for L in got:
+                    while (r := node.take_frame(L)) is not None:
+                        got[L].append(r)
+        node.flush()
+        for L in got:
+            while (r := node.take_frame(L)) is not None:
+                got[L].append(r)
+    finally:
+        node.close()
+    want = _oracle_levels(oracle, geo, dtype, method, frames)
+    for L in got:
+        assert len(got[L]) == len(want[L]), (i, dims, devices, L)
+        for k, (a, b) in enumerate(zip(got[L], want[L])):
+            assert_parity(a, b, f"fuzz {i} {dims} L{L} frame {k}")
