@@ -832,7 +832,7 @@ def measure_traffic(args, kernel):
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
                "--workload", args.workload, "--batch", str(args.batch),
-               "--method", args.method, "--steps", "3", "--warmup", "1"]
+               "--method", args.method, "--steps", "3", "--warmup", "1", "--no-check"]
         if args.tiled:
             cmd.append("--tiled")
         if args.no_flags:
@@ -854,11 +854,18 @@ def measure_traffic(args, kernel):
         with open(files[0]) as f:
             for row in csv.DictReader(f):
                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                    per.append(float(row["Counter_Value"]))
+                    per.append((int(row.get("Dispatch_Id") or len(per)),
+                                float(row["Counter_Value"])))
         shutil.rmtree(d, ignore_errors=True)
         if not per:
             return None
-        vals[counter] = float(np.mean(per[1:] if len(per) > 1 else per))
+        # the child runs 1 warm-up + 3 timed steps; a step of a deep pyramid
+        # is several launches (levels 5+ chain a second one): sum per step,
+        # average over the timed steps
+        per = [v for _, v in sorted(per)]
+        k = max(1, len(per) // 4)
+        steps = [sum(per[i:i + k]) for i in range(0, len(per) - len(per) % k, k)]
+        vals[counter] = float(np.mean(steps[1:] if len(steps) > 1 else steps))
     fetch = vals["FETCH_SIZE"] * 1024 * 2
     write = vals["WRITE_SIZE"] * 1024
     return {"bytes_per_launch": int(fetch + write), "read_bytes": int(fetch),

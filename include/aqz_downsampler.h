@@ -596,6 +596,7 @@ typedef struct aqz_node aqz_node;
 /*
  * One aqz_ds handle per entry of `devices` (HIP ordinals; an ordinal may
  * repeat, giving several handles on one GPU).  Validation as aqz_ds_create.
+ * Like an aqz_ds, a node serves one caller thread at a time.
  */
 int aqz_node_create(const aqz_level_desc* levels,
                     uint32_t n_levels,
