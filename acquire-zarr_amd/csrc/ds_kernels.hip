@@ -366,7 +366,7 @@ struct CascadeParams
     TiledLevel tl[kMaxFusedLevels];
     uint32_t zitems;                 // items per frame, all levels
     FastDiv zdiv;                    // by zitems
-    uint32_t zwaves;                 // zero-fill waves: the grid's first zwaves / 4 blocks
+    uint32_t zwaves;                 // zero-fill waves: the grid's first zwaves / (waves per block) blocks
     uint32_t main_blocks;            // blocks of cascade waves after them
     uint32_t remap;                  // 1: XCD-contiguous block order (cascade_kernel)
     uint32_t wb;                     // bit J-1: level J's row-major stores write-back, not nt
@@ -1044,9 +1044,10 @@ cascade_kernel(CascadeParams p)
     if constexpr (TILED) {
         // The first blocks zero-fill the tile overhang (dispatched round-robin
         // over the XCDs like any blocks); the cascade blocks follow.
-        const uint32_t zb = p.zwaves / 4;
+        const uint32_t wpb = blockDim.x >> 6;
+        const uint32_t zb = p.zwaves / wpb;
         if (blk < zb) {
-            zero_fill_tiled<T>(p, blk * 4 + wave, p.zwaves, lane, NL,
+            zero_fill_tiled<T>(p, blk * wpb + wave, p.zwaves, lane, NL,
                                p.total_units / (p.units_x * p.units_y));
             return;
         }
@@ -1066,13 +1067,26 @@ cascade_kernel(CascadeParams p)
         // one unit per wave (the loop below, even run once, cost the tiled
         // instantiations 40-70% more VGPRs: headline 60 -> 100, half the
         // occupancy, 3000^2 tiled 539 -> 710 us)
-        const uint32_t u = blk * (blockDim.x >> 6) + wave;
-        if (u >= p.total_units)
-            return;
-        const uint32_t ux = u % p.units_x;
-        const uint32_t t = u / p.units_x;
-        const uint32_t uy = t % p.units_y;
-        const uint32_t f = t / p.units_y;
+        uint32_t ux, uy, f;
+        if (p.seg_w) {
+            // band-aligned workgroups (rows that split 128-B lines): the
+            // waves sharing a line run on one CU, so it is fetched once
+            const uint32_t segs = (p.units_x + p.seg_w - 1) / p.seg_w;
+            const uint32_t band = blk / segs;
+            ux = (blk - band * segs) * p.seg_w + wave;
+            if (ux >= p.units_x || band >= p.total_units / p.units_x)
+                return;
+            uy = band % p.units_y;
+            f = band / p.units_y;
+        } else {
+            const uint32_t u = blk * (blockDim.x >> 6) + wave;
+            if (u >= p.total_units)
+                return;
+            ux = u % p.units_x;
+            const uint32_t t = u / p.units_x;
+            uy = t % p.units_y;
+            f = t / p.units_y;
+        }
         const uint32_t row0 = uy * R;
         const uint32_t tile_col0 = ux * (64u * C);
         const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
@@ -2471,11 +2485,29 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
                  : 0u;
     if (const int zw = tiled_zwaves_env(); zw >= 0)
         p.zwaves = uint32_t(zw); // A/B only: 0 leaves the overhang unwritten
-    p.zwaves = (p.zwaves + 31) & ~31u;
-    p.main_blocks = grid_for(total, 4, 0);
     p.remap = xcd_remap_env() == 1;
     p.nt = load_nt(W, b);
-    const uint32_t grid = p.zwaves / 4 + p.main_blocks;
+    // $AQZ_TILED_BAND_WG=1 (A/B, off by default): on rows that split 128-B
+    // lines, one workgroup per row band (or balanced piece of <= 8 tiles), as
+    // the row-major launcher does, so that the two waves sharing a line read
+    // it through one L2.  Reads drop to 1.00-1.01x the frame (from 1.02-1.05x)
+    // but every shape got slower: u16 3000^2 543 -> 615 us, 5472x3648 517 ->
+    // 610, 6000x4000 503 -> 597, 2000^2 507 -> 511, f32 6000x4000 990 -> 1111
+    // (same box, two rounds, profiles/r04/tiledwg/).
+    static const bool band_wg = int_env("AQZ_TILED_BAND_WG", 0) != 0;
+    uint32_t wpb = 4;
+    if (band_wg && !p.remap && (uint64_t(W) * b) % 128 != 0 && p.units_x > 1) {
+        const uint32_t nseg = (p.units_x + 7) / 8;
+        p.seg_w = (p.units_x + nseg - 1) / nseg;
+        wpb = p.seg_w;
+        p.main_blocks = nseg * p.units_y * n_frames;
+    } else {
+        p.main_blocks = grid_for(total, 4, 0);
+    }
+    // zero-fill blocks: a whole number of 8-block (one per XCD) groups
+    const uint32_t zblocks = ((p.zwaves + wpb - 1) / wpb + 7) & ~7u;
+    p.zwaves = zblocks * wpb;
+    const uint32_t grid = zblocks + p.main_blocks;
 
     return with_dtype(dtype, [&](auto tag) -> hipError_t {
         using T = decltype(tag);
@@ -2490,19 +2522,19 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
                 switch (n_out) {
                     case 1:
                         hipLaunchKernelGGL((cascade_kernel<T, M, 1, C, NT, MD>), dim3(grid),
-                                           dim3(256), 0, stream, p);
+                                           dim3(64 * wpb), 0, stream, p);
                         break;
                     case 2:
                         hipLaunchKernelGGL((cascade_kernel<T, M, 2, C, NT, MD>), dim3(grid),
-                                           dim3(256), 0, stream, p);
+                                           dim3(64 * wpb), 0, stream, p);
                         break;
                     case 3:
                         hipLaunchKernelGGL((cascade_kernel<T, M, 3, C, NT, MD>), dim3(grid),
-                                           dim3(256), 0, stream, p);
+                                           dim3(64 * wpb), 0, stream, p);
                         break;
                     default:
                         hipLaunchKernelGGL((cascade_kernel<T, M, 4, C, NT, MD>), dim3(grid),
-                                           dim3(256), 0, stream, p);
+                                           dim3(64 * wpb), 0, stream, p);
                         break;
                 }
             };
