@@ -825,6 +825,33 @@ def test_add_frame_async_errors(aqz):
     ds.close()  # destroy settles the pending add
 
 
+def test_add_frame_async_take_checks_buffers_first(aqz, oracle):
+    """every take buffer is checked before the background job is
+    queued — a level-2 buffer too small fails the call with nothing queued,
+    so level 1 is not taken (and lost) either; the same frame then goes
+    through with proper buffers and matches the oracle."""
+    import ctypes
+    geo = halving_geometry(128, 96, 3)
+    ds = aqz.Downsampler(geo, np.uint16, aqz.MEAN)
+    frame = np.arange(128 * 96, dtype=np.uint16).reshape(96, 128)
+    L = aqz.lib()
+    takes = (aqz.LevelTake * 3)()
+    b1 = np.empty((48, 64), np.uint16)
+    b2 = np.empty(10, np.uint16)                     # level 2 needs 24 x 32
+    takes[1] = aqz.LevelTake(aqz.TAKE_INTO, 0, 0, b1.ctypes.data, b1.nbytes, None, 0, 0)
+    takes[2] = aqz.LevelTake(aqz.TAKE_INTO, 0, 0, b2.ctypes.data, b2.nbytes, None, 0, 0)
+    rc = L.aqz_ds_add_frame_async_take(ds._h, frame.ctypes.data, frame.nbytes, takes)
+    assert rc == 1 and b"take buffer" in L.aqz_ds_last_error(ds._h)
+    assert L.aqz_ds_wait(ds._h) == 0                 # nothing was queued
+    assert ds.take_frame(1) is None                  # and nothing was added
+    ds.add_frame_async_take(frame, None)
+    got = ds.wait_takes()
+    ref = oracle.cascade_2d(frame, 3, aqz.MEAN)
+    for lv in (1, 2):
+        np.testing.assert_array_equal(got[lv], ref[lv - 1])
+    ds.close()
+
+
 # ---- §8(f) row 2: transposed storage order and level-0 take -----------------
 
 TRANSPOSE_SHAPES = [(64, 64), (4096, 4096), (1000, 777), (129, 4100), (1, 5), (5, 1),
