@@ -1,8 +1,9 @@
 """Full-size parity against committed digests: every BASELINE config x method
 through the HIP path, both the streaming drop-in (add_frame / take_frame)
 and the device-resident batch (run_device_batch, the bench path), must hash
-to the oracle's per-level SHA-256 (tests/golden/config_digests.json).  No
-oracle runs here, so the sizes are the real ones."""
+to the per-level SHA-256 the REFERENCE ITSELF produced
+(tests/golden/reference_digests.json, oracle/_ref).  No CPU code runs here,
+so the sizes are the real ones."""
 import hashlib
 import json
 

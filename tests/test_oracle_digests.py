@@ -1,7 +1,9 @@
 """The oracle reproduces the committed per-level digests of every BASELINE
-config x method at full size (tests/golden/config_digests.json, made by
-tests/golden/make_digests.py).  A regression guard for the oracle; the GPU
-path is held to the same digests in tests/test_gpu_digests.py."""
+config x method at full size — tests/golden/reference_digests.json, made by
+the REFERENCE ITSELF (oracle/_ref, tests/golden/make_reference_vectors.py
+--digests).  The GPU path is held to the same digests in
+tests/test_gpu_digests.py; the oracle's own copy (config_digests.json,
+make_digests.py) equals them (tests/test_reference_pin.py)."""
 import json
 
 import pytest
