@@ -30,7 +30,7 @@ def _host(nbytes):
     return np.empty(max(nbytes, 1), np.uint8)
 
 
-@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["x2", "x3"])
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0] * 8], ids=["x2", "x3", "x8"])
 @pytest.mark.parametrize("dtype", [np.uint16, np.float32, np.uint8], ids=lambda d: np.dtype(d).name)
 @pytest.mark.parametrize("name", list(CASES))
 def test_node_host_batch_matches_oracle(aqz, oracle, name, dtype, devices):
@@ -111,7 +111,7 @@ STREAM_CASES = {
 }
 
 
-@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["x2", "x3"])
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0] * 8], ids=["x2", "x3", "x8"])
 @pytest.mark.parametrize("dtype", [np.uint16, np.float32], ids=lambda d: np.dtype(d).name)
 @pytest.mark.parametrize("name", list(STREAM_CASES))
 def test_node_stream_matches_oracle(aqz, oracle, name, dtype, devices):
