@@ -555,6 +555,24 @@ def main():
         e2e_multi["pcie_GBps"] = round(e2e_multi["pcie_GBps"] * world, 1)
         e2e_multi["path"] += f", all {world} ranks at once (aggregate, max-over-ranks time)"
         e2e = {"pipelined_all_ranks": e2e_multi}
+        # the library's own node sharding (aqz_node): ONE process
+        # dealing host frames over all the ranks' GPUs, each over its own PCIe
+        # link.  The other ranks wait on a CPU-only group meanwhile, so no
+        # collective kernel spins on their GPUs.
+        cpu_group = dist.new_group(backend="gloo")
+        if rank == 0:
+            n_vis = torch.cuda.device_count()
+            # a gloo rehearsal on a smaller box repeats ordinals, as the ranks do
+            rehearsal = n_vis < world and os.environ.get("AQZ_DIST_BACKEND") == "gloo"
+            if n_vis >= world or rehearsal:
+                e2e["node"] = measure_e2e_node(aqz, torch, geo, dtype, method, d_in,
+                                               min(B, 64), [r % n_vis for r in range(world)])
+                if rehearsal:
+                    e2e["node"]["rehearsal"] = f"{world} handles on {n_vis} device(s)"
+            else:
+                e2e["node"] = {"skipped": f"{n_vis} device(s) visible to rank 0, "
+                                          f"{world} needed"}
+        dist.barrier(group=cpu_group)
 
     if rank == 0:
         metric = HEADLINE_METRIC if (args.workload == "4096x4096_u16" and not args.shape
