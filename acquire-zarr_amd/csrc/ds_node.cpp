@@ -431,6 +431,18 @@ aqz_node_run_host_batch(aqz_node* n,
         std::vector<int> rc(D, AQZ_OK);
         std::vector<std::vector<uint32_t>> counts(D, std::vector<uint32_t>(nl, 0));
         std::vector<std::thread> workers;
+        // joins whatever started, also when a thread fails to start or the
+        // caller's share throws, so no joinable thread is ever destroyed
+        struct JoinAll
+        {
+            std::vector<std::thread>& t;
+            ~JoinAll()
+            {
+                for (auto& w : t)
+                    if (w.joinable())
+                        w.join();
+            }
+        } join_all{ workers };
         auto run = [&](uint32_t d) {
             const uint32_t u0 = first[d], nu = first[d + 1] - first[d];
             if (nu == 0)
