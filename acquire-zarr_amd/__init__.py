@@ -38,7 +38,7 @@ EXPORTS = (
     "aqz_ds_last_batch_kind", "aqz_ds_stream_tiled_runs", "aqz_ds_run_host_batch", "aqz_ds_take_frame_tiled",
     "aqz_ds_run_device_batch_tiled", "aqz_ds_tiled_flag_slots",
     "aqz_tile_frame_device", "aqz_ds_set_level_tiling",
-    "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_add_frame_async_take", "aqz_ds_set_input_transpose",
+    "aqz_ds_add_frame_async", "aqz_ds_wait", "aqz_ds_poll", "aqz_ds_add_frame_async_take", "aqz_ds_set_input_transpose",
     "aqz_ds_take_input_frame", "aqz_transpose_frame_device",
     "aqz_blosc_filter_device", "aqz_crc32c_device", "aqz_tile_slices",
     "aqz_tile_frame_device_sliced",
@@ -132,6 +132,7 @@ def lib() -> ctypes.CDLL:
     L.aqz_ds_add_frame_async.argtypes = [vp, vp, sz]
     L.aqz_ds_add_frame_async_take.argtypes = [vp, vp, sz, ctypes.POINTER(LevelTake)]
     L.aqz_ds_wait.argtypes = [vp]
+    L.aqz_ds_poll.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.aqz_ds_set_input_transpose.argtypes = [vp, ctypes.c_int]
     L.aqz_ds_take_input_frame.argtypes = [vp, u32, u32, vp, sz, vp, ctypes.POINTER(sz),
                                           ctypes.POINTER(ctypes.c_int)]
@@ -407,6 +408,12 @@ class Downsampler:
             self._check(lib().aqz_ds_wait(self._h))
         finally:
             self._pending = None
+
+    def poll(self) -> bool:
+        """aqz_ds_poll: True once no add_frame_async job is running."""
+        done = ctypes.c_int(0)
+        self._check(lib().aqz_ds_poll(self._h, ctypes.byref(done)))
+        return bool(done.value)
 
     def add_frame_async_take(self, frame: np.ndarray, tiles, hold=()):
         """aqz_ds_add_frame_async_take: every level L >= 1 taken in the

@@ -145,6 +145,29 @@ publish(aqz_node* n)
     }
 }
 
+// Settle, without waiting, the adds at the front of the submission order
+// whose background job has finished: their levels can be handed out now
+// rather than when their handle is next used.  Stops at the first add still
+// running, since later adds publish only after it anyway.
+int
+settle_finished(aqz_node* n)
+{
+    for (auto& a : n->adds) {
+        if (a.settled)
+            continue;
+        if (n->in_flight[a.handle] != &a)
+            break;
+        int done = 0;
+        if (int rc = aqz_ds_poll(n->ds[a.handle], &done))
+            return fail(n, rc, "node take: poll failed");
+        if (!done)
+            break;
+        if (int rc = settle_handle(n, a.handle))
+            return rc;
+    }
+    return AQZ_OK;
+}
+
 int
 flush_all(aqz_node* n)
 {
@@ -348,6 +371,8 @@ aqz_node_take_frame(aqz_node* n,
             *nbytes = 0;
         if (level == 0 || level >= n->lv.size())
             return AQZ_OK;
+        if (int rc = settle_finished(n))
+            return rc;
         publish(n);
         auto& q = n->ready[level];
         if (q.empty())

@@ -1338,6 +1338,24 @@ aqz_ds_wait(aqz_ds* ds)
 }
 
 int
+aqz_ds_poll(aqz_ds* ds, int* done)
+{
+    try {
+        if (!ds || !done)
+            return AQZ_INVALID_ARGUMENT;
+        *done = 1;
+        auto& a = ds->async;
+        if (a.worker.joinable()) {
+            std::lock_guard<std::mutex> lk(a.m);
+            *done = a.frame == nullptr;
+        }
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
+}
+
+int
 aqz_ds_add_device_frame(aqz_ds* ds, const void* device_frame, size_t nbytes)
 {
     try {

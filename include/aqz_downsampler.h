@@ -185,6 +185,15 @@ int aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes);
 int aqz_ds_wait(aqz_ds* ds);
 
 /*
+ * Non-blocking: *done = 1 when no aqz_ds_add_frame_async job is running (the
+ * next aqz_ds_wait returns at once), 0 while one is.  Reports nothing else and
+ * clears no status: the job's status is still aqz_ds_wait's to return.  No
+ * reference counterpart; aqz_node_take_frame uses it to hand out levels as
+ * soon as their add has finished.
+ */
+int aqz_ds_poll(aqz_ds* ds, int* done);
+
+/*
  * One level's part in aqz_ds_add_frame_async_take.
  *   mode AQZ_TAKE_NONE: nothing (the level is taken later, or not at all);
  *   AQZ_TAKE_INTO: right behind the add, take the level's frame if it has
@@ -643,8 +652,9 @@ int aqz_node_add_frame(aqz_node* node, const void* host_frame, size_t nbytes);
 
 /*
  * The next level-`level` frame in emission order, if its add has completed
- * (non-blocking: *has_frame = 0 when none is ready yet; aqz_node_flush makes
- * every frame of the adds so far ready).  `dst` NULL: size query, the frame
+ * (non-blocking: finished adds are settled through aqz_ds_poll, and
+ * *has_frame = 0 when the frame's add, or an earlier one, still runs;
+ * aqz_node_flush makes every frame of the adds so far ready).  `dst` NULL: size query, the frame
  * stays queued.
  */
 int aqz_node_take_frame(aqz_node* node,

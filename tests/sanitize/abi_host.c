@@ -132,6 +132,9 @@ main(void)
             aqz_node_take_frame(NULL, 1, NULL, 0, NULL, &has) != AQZ_INVALID_ARGUMENT ||
             aqz_node_flush(NULL) != AQZ_INVALID_ARGUMENT)
             return 28;
+        int done = 0;
+        if (aqz_ds_poll(NULL, &done) != AQZ_INVALID_ARGUMENT)
+            return 29;
     }
     printf("abi_host: ok (%s; %s)\n", aqz_version(), aqz_blosc_codec_info());
     return 0;

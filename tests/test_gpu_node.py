@@ -248,3 +248,55 @@ def test_node_fuzz(aqz, oracle, i):
         assert len(got[L]) == len(want[L]), (i, dims, devices, L)
         for k, (a, b) in enumerate(zip(got[L], want[L])):
             assert_parity(a, b, f"fuzz {i} {dims} L{L} frame {k}")
+
+
+def test_node_take_hands_out_finished_adds_early(aqz, oracle):
+    """aqz_node_take_frame settles, without waiting, every add whose
+    background job has finished (aqz_ds_poll), so a frame's levels come out
+    before its handle is used again — here without any later add or flush."""
+    import time
+    dims = STREAM_CASES["2d_1000x600"][0]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    node = aqz.Node(geo, np.uint16, aqz.MEAN, [0, 0, 0])
+    w, h, _ = geo[0]
+    frames = random_frames(np.random.default_rng(9), np.uint16, (2, h, w))
+    try:
+        for f in frames:
+            node.add_frame(f)
+        got = {L: [] for L in range(1, len(geo))}
+        deadline = time.monotonic() + 20
+        while any(len(v) < 2 for v in got.values()) and time.monotonic() < deadline:
+            for L in got:
+                while (r := node.take_frame(L)) is not None:
+                    got[L].append(r)
+            time.sleep(0.001)
+        assert all(len(v) == 2 for v in got.values()), {L: len(v) for L, v in got.items()}
+        node.flush()
+        for L in got:
+            assert node.take_frame(L) is None
+    finally:
+        node.close()
+    want = _oracle_levels(oracle, geo, np.uint16, aqz.MEAN, frames)
+    for L in got:
+        for k, (a, b) in enumerate(zip(got[L], want[L])):
+            assert_parity(a, b, f"early L{L} frame {k}")
+
+
+def test_poll_reports_the_async_job(aqz):
+    """aqz_ds_poll: done with nothing pending, done again once the add
+    finishes, and it leaves the job's status to aqz_ds_wait."""
+    import time
+    geo = [(256, 256, 1), (128, 128, 1)]
+    ds = aqz.Downsampler(geo, np.uint16, aqz.MEAN)
+    try:
+        assert ds.poll()
+        frame = np.arange(256 * 256, dtype=np.uint16).reshape(256, 256)
+        ds.add_frame_async(frame)
+        deadline = time.monotonic() + 20
+        while not ds.poll() and time.monotonic() < deadline:
+            time.sleep(0.001)
+        assert ds.poll()
+        ds.wait()
+        assert ds.take_frame(1) is not None
+    finally:
+        ds.close()
