@@ -2503,7 +2503,17 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         wpb = p.seg_w;
         p.main_blocks = nseg * p.units_y * n_frames;
     } else {
-        p.main_blocks = grid_for(total, 4, 0);
+        // Waves per workgroup: 4 when a row band's tile count divides by 4,
+        // else 2.  Same box, two rounds (profiles/r04/tiledwaves/): u16
+        // 3000^2 541-549 -> 518-521 us, 2304^2 614-621 -> 576-577, 3500^2
+        // 552 -> 519, 4600x3000 531 -> 510, f32 5472x3648 1191-1193 -> 1116-
+        // 1118, u8 6000x4000 89-96 -> 80-85; but 2-wave blocks lose where 4
+        // divide the band (u16 2000^2 505 -> 580, 6000x4000 505 -> 546-550,
+        // f32 6000x4000 989 -> 1063), and 3-wave blocks lose on 6 tiles
+        // (3000^2 574-576).  $AQZ_TILED_WAVES (1..8) forces a count (A/B).
+        static const int tw = int_env("AQZ_TILED_WAVES", 0);
+        wpb = tw > 0 ? uint32_t(std::min(tw, 8)) : (p.units_x % 4 == 0 ? 4u : 2u);
+        p.main_blocks = grid_for(total, wpb, 0);
     }
     // zero-fill blocks: a whole number of 8-block (one per XCD) groups
     const uint32_t zblocks = ((p.zwaves + wpb - 1) / wpb + 7) & ~7u;
