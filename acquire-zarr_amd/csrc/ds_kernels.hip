@@ -2346,6 +2346,10 @@ cascade_tiled_cols(int dtype, uint32_t W)
     if (!b)
         return 0;
     const uint32_t cw = cascade_cols(b);
+    // $AQZ_TILED_NARROW (A/B): 1 half-width tiles wherever they fit, 0 wide
+    static const int narrow = int_env("AQZ_TILED_NARROW", -1);
+    if (narrow == 1 && W >= 64 * (cw / 2))
+        return cw / 2;
     return W >= 64 * cw ? cw : cw / 2;
 }
 
@@ -2395,11 +2399,14 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
                                   uint32_t n_frames,
                                   hipStream_t stream)
 {
-    const uint32_t cols = cascade_pick_cols(dtype, src, src_frame_elems, W, H, outs, n_out);
-    // the flag layout (cascade_tiled_slots) assumes the geometry-only choice
-    if (cols == 0 || n_frames == 0 || cols != cascade_tiled_cols(dtype, W))
-        return hipErrorInvalidValue;
+    // the flag layout (cascade_tiled_slots) assumes the geometry-only choice;
+    // cascade_pick_cols != 0 says the buffers and level sizes fit the fused
+    // cascade (its conditions do not depend on the tile width)
+    const uint32_t cols = cascade_tiled_cols(dtype, W);
     const size_t b = dtype_bytes(dtype);
+    if (cols == 0 || n_frames == 0 ||
+        cascade_pick_cols(dtype, src, src_frame_elems, W, H, outs, n_out) == 0)
+        return hipErrorInvalidValue;
     const uint32_t R = 1u << n_out;
     CascadeParams p{};
     p.src = static_cast<const uint8_t*>(src);
@@ -2481,8 +2488,21 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         zbytes += (uint64_t(q.pw) * q.ph - cw * chh) * b;
     }
     zbytes *= n_frames;
+    // ... and for 1-byte types at most ZI = 32 overhang rows per wave: each
+    // row is a short dependent loop, and the byte rule left u8 pyramids
+    // (chunk 128, rows of a few dozen bytes) with thousands of rows per
+    // wave, the kernel's tail.  Same box (profiles/r04/zrows/ab.log): u8
+    // 2600^2 262 -> 111 us, 2304^2 273 -> 131, 1500^2 189 -> 113, 3000^2
+    // 141 -> 93, 5000x4000 100 -> 81; the same cap cost u16 2-4% (3000^2
+    // 516-519 -> 528-531 us), so wider types keep the byte rule.
+    // $AQZ_TILED_ZROWS_PER_WAVE: ZI for every type (0: the byte rule alone).
+    static const int zi_env = int_env("AQZ_TILED_ZROWS_PER_WAVE", -1);
+    const int zi = zi_env >= 0 ? zi_env : (b == 1 ? 32 : 0);
+    uint64_t zw = (zbytes >> 17) + 1;
+    if (zi > 0)
+        zw = std::max<uint64_t>(zw, (zitems + zi - 1) / uint64_t(zi));
     p.zwaves = (zitems || flag_fill)
-                 ? uint32_t(std::min<uint64_t>(std::max<uint64_t>((zbytes >> 17) + 1, 64), 4096))
+                 ? uint32_t(std::min<uint64_t>(std::max<uint64_t>(zw, 64), 4096))
                  : 0u;
     if (const int zw = tiled_zwaves_env(); zw >= 0)
         p.zwaves = uint32_t(zw); // A/B only: 0 leaves the overhang unwritten
