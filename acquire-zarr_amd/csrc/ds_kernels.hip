@@ -72,12 +72,80 @@ enum
 
 // ---- reducers --------------------------------------------------------------
 
+// NaN payloads exactly as the reference binary makes them.  IEEE 754 leaves
+// a NaN result's payload open; the reference's compiled float mean (x86 SSE
+// addss/divss, downsampler.cpp:48-51,108-112) returns the FIRST source
+// operand's NaN, quieted, when it is a NaN, else the second's, and for an
+// invalid sum (inf + -inf) the negative "default NaN" (sign and quiet bits
+// set, zero payload).  gfx950's v_add/v_div pick differently (inf - inf
+// gives the positive quiet NaN), so the kernels keep
+// the plain arithmetic and rebuild the bits only where the result is a NaN:
+// one compare per output in the common case, the walk below when a wave has
+// a NaN lane.  The walk works on bits (integer ops) so nothing canonicalises
+// the payload; divide by 4 or 2 keeps a quiet NaN unchanged on x86.  The
+// oracle states the same rule (oracle/ds_oracle.c add_<T>).
+template<typename T>
+struct float_bits;
+template<>
+struct float_bits<float>
+{
+    using U = uint32_t;
+    static constexpr U quiet = 0x00400000u;
+    static constexpr U default_nan = 0xFFC00000u;
+};
+template<>
+struct float_bits<double>
+{
+    using U = uint64_t;
+    static constexpr U quiet = 0x0008000000000000ull;
+    static constexpr U default_nan = 0xFFF8000000000000ull;
+};
+
+// x86 `x + y` with its NaN rule (x the first source).
+template<typename T>
+__device__ __forceinline__ T
+x86_add(T x, T y)
+{
+    using FB = float_bits<T>;
+    using U = typename FB::U;
+    const T s = x + y;
+    U r;
+    if (x != x)
+        r = __builtin_bit_cast(U, x) | FB::quiet;
+    else if (y != y)
+        r = __builtin_bit_cast(U, y) | FB::quiet;
+    else if (s != s)
+        r = FB::default_nan;
+    else
+        return s;
+    return __builtin_bit_cast(T, r);
+}
+
+template<typename T>
+__device__ __forceinline__ T
+mean4_nan(T a, T b, T c, T d)
+{
+    // a NaN result: the chain's first NaN is its value (x86 keeps it through
+    // the later adds and the divide)
+    return x86_add(x86_add(x86_add(a, b), c), d);
+}
+
+template<typename T>
+__device__ __forceinline__ T
+mean2_nan(T a, T b)
+{
+    return x86_add(a, b);
+}
+
 template<typename T>
 __device__ __forceinline__ T
 mean4(T a, T b, T c, T d)
 {
     if constexpr (std::is_floating_point_v<T>) {
-        return (((a + b) + c) + d) / T(4);
+        const T r = (((a + b) + c) + d) / T(4);
+        if (__builtin_expect(r != r, 0))
+            return mean4_nan(a, b, c, d);
+        return r;
     } else if constexpr (sizeof(T) < sizeof(int)) {
         return T((int(a) + int(b) + int(c) + int(d)) / 4);
     } else {
@@ -92,7 +160,10 @@ __device__ __forceinline__ T
 mean2(T a, T b)
 {
     if constexpr (std::is_floating_point_v<T>) {
-        return (a + b) / T(2);
+        const T r = (a + b) / T(2);
+        if (__builtin_expect(r != r, 0))
+            return mean2_nan(a, b);
+        return r;
     } else if constexpr (sizeof(T) < sizeof(int)) {
         return T((int(a) + int(b)) / 2);
     } else {

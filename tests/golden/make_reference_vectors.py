@@ -3,6 +3,7 @@
     make -C oracle ref                                   # builds oracle/_ref
     python tests/golden/make_reference_vectors.py        # vectors + manifest
     python tests/golden/make_reference_vectors.py --digests   # + BASELINE digests
+    python tests/golden/make_reference_vectors.py --nan-only  # NaN-payload set only
 
 Every output byte here comes from acquire-zarr v0.8.1's own
 zarr::Downsampler / ArrayDimensions (src/streaming/downsampler.cpp,
@@ -87,6 +88,36 @@ def vectors():
     print("wrote", rv.NPZ, os.path.getsize(rv.NPZ), "bytes")
 
 
+def nan_vectors():
+    """The NaN-payload cases (refvec.NAN_GEOMETRIES x float dtypes x methods),
+    same layout as the main vectors; geometries come from the main manifest."""
+    arrays = {}
+    for gi, geom in enumerate(rv.NAN_GEOMETRIES):
+        dims, n_frames, take = rv.GEOMETRIES[geom]
+        for di, dt in enumerate(rv.NAN_DTYPES):
+            dname = np.dtype(dt).name
+            x = rv.make_nan_inputs(geom, dt, SEED + 7000 + 100 * gi + di)
+            arrays[f"in/{geom}/{dname}"] = x
+            for m in range(4):
+                ds = ref.RefDownsampler(dims, dt, m)
+                ev, out = [], []
+                for k in range(n_frames):
+                    ds.add_frame(x[k])
+                    if not rv.take_now(take, k):
+                        continue
+                    for L in range(1, ds.n_levels):
+                        b = ds.take_bytes(L)
+                        ev.append((k, L, b is not None, 0 if b is None else b.size))
+                        if b is not None:
+                            out.append(b)
+                name = rv.case_name(geom, dt, m)
+                arrays[f"ev/{name}"] = np.array(ev, dtype=np.int64).reshape(-1, 4)
+                arrays[f"out/{name}"] = (np.concatenate(out) if out
+                                         else np.zeros(0, np.uint8))
+    np.savez_compressed(rv.NAN_NPZ, **arrays)
+    print("wrote", rv.NAN_NPZ, os.path.getsize(rv.NAN_NPZ), "bytes")
+
+
 def digests():
     out = {"generator": "tests/digest_util.py (splitmix64, seed 0xA0C2A11 + sorted config index)",
            "digest": "sha256 of each level's taken frames, concatenated in order",
@@ -114,9 +145,14 @@ def digests():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--digests", action="store_true", help="also the BASELINE-config digests")
+    ap.add_argument("--nan-only", action="store_true",
+                    help="only the NaN-payload vectors (reference_nan_vectors.npz)")
     a = ap.parse_args()
     if not ref.build():
         sys.exit("oracle/_ref is not built and /root/reference is absent")
+    nan_vectors()
+    if a.nan_only:
+        return
     vectors()
     if a.digests:
         digests()

@@ -47,8 +47,9 @@ def random_frames(rng, dtype, shape, specials=True):
 
 
 def assert_parity(got, want, ctx=""):
-    """Bit-exact for integers; float32/64 within 1 ulp (NaN positions must
-    match) — the tolerance north_star states.  The kernels are expected to be
+    """Bit-exact for integers; float32/64 within 1 ulp — the tolerance
+    north_star states — with NaNs at the same positions carrying the same bits
+    (the reference binary's payloads).  The kernels are expected to be
     bit-exact; `exact_fraction` is reported on failure."""
     assert got.shape == want.shape, f"{ctx}: shape {got.shape} vs {want.shape}"
     assert got.dtype == want.dtype
@@ -61,6 +62,8 @@ def assert_parity(got, want, ctx=""):
         return
     gn, wn = np.isnan(got), np.isnan(want)
     assert np.array_equal(gn, wn), f"{ctx}: NaN positions differ"
+    ib = np.dtype(f"u{got.dtype.itemsize}")
+    assert np.array_equal(got[gn].view(ib), want[wn].view(ib)), f"{ctx}: NaN payloads differ"
     g, w = got[~gn], want[~wn]
     ok = (g == w)
     if not ok.all():

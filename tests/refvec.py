@@ -31,6 +31,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 NPZ = os.path.join(GOLDEN, "reference_vectors.npz")
 MANIFEST = os.path.join(GOLDEN, "reference_vectors.json")
 DIGESTS = os.path.join(GOLDEN, "reference_digests.json")
+NAN_NPZ = os.path.join(GOLDEN, "reference_nan_vectors.npz")
 
 NP_DTYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16,
              np.int32, np.int64, np.float32, np.float64]
@@ -105,6 +106,50 @@ def make_inputs(geom, dtype, seed):
         x[:, :2, :2] = ii.max        # 4*max wraps in 32/64-bit arithmetic
         x[:, :2, 2:4] = ii.min
     return x
+
+
+# NaN-payload cases (reference_nan_vectors.npz): the float dtypes over
+# geometries that exercise mean4 with replicated edge operands (odd XY) and
+# mean2 (Z pairs), on inputs dense in NaNs of every sign, payload and
+# quietness, so the reference binary's NaN choice (first NaN operand,
+# quieted; the negative default NaN for inf - inf) is pinned byte for byte.
+NAN_GEOMETRIES = ["xy_odd_37x29", "z7_9x7", "c2_z5_10x12"]
+NAN_DTYPES = [np.float32, np.float64]
+
+
+def make_nan_inputs(geom, dtype, seed):
+    """Frames whose elements are, in about equal parts, quiet NaNs, signaling
+    NaNs (random sign and nonzero payload), +inf, -inf and ordinary values.
+    Built on the bit patterns, so nothing on the way quiets a NaN."""
+    dims, n_frames, _ = GEOMETRIES[geom]
+    h, w = dims[-2][1], dims[-1][1]
+    dt = np.dtype(dtype)
+    ut = np.dtype(f"u{dt.itemsize}")
+    nbits = 8 * dt.itemsize
+    mant = 23 if dt.itemsize == 4 else 52
+    rng = np.random.default_rng(seed)
+    shape = (n_frames, h, w)
+    x = (rng.standard_normal(shape) * 1e3).astype(dt)
+    bits = x.view(ut).reshape(-1)
+    kind = rng.integers(0, 5, bits.size)
+    exp = ut.type(((1 << (nbits - 1 - mant)) - 1) << mant)
+    sign = rng.integers(0, 2, bits.size).astype(ut) << ut.type(nbits - 1)
+    quiet = ut.type(1 << (mant - 1))
+    payload = rng.integers(1, 1 << (mant - 1), bits.size, dtype=np.uint64).astype(ut)
+    qnan = sign | exp | quiet | (payload & ut.type(0xFF if mant == 23 else 0xFFFF))
+    snan = sign | exp | payload               # quiet bit clear, payload nonzero
+    inf = np.array(np.inf, dt).view(ut)
+    ninf = np.array(-np.inf, dt).view(ut)
+    bits[kind == 0] = qnan[kind == 0]
+    bits[kind == 1] = snan[kind == 1]
+    bits[kind == 2] = inf
+    bits[kind == 3] = ninf
+    return bits.view(dt).reshape(shape)
+
+
+def nan_cases():
+    return [(g, np.dtype(d).name, m) for g in NAN_GEOMETRIES for d in NAN_DTYPES
+            for m in range(len(METHOD_NAMES))]
 
 
 def load():

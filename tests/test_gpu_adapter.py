@@ -20,7 +20,9 @@ the patched write_frame):
 
 Every take is compared with the frames the REFERENCE ITSELF made for the same
 inputs (tests/golden/reference_vectors.*), row-major or tiled by the oracle's
-tile_frame (array.cpp:507-622).  Floats: NaN positions and every other bit.
+tile_frame (array.cpp:507-622).  Byte for byte, float NaN payloads included;
+the float Mean cases also replay the NaN-payload set
+(tests/golden/reference_nan_vectors.npz).
 """
 import os
 import subprocess
@@ -35,6 +37,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "tests", "cpp", "bin", "adapter_harness")
 MAN, VEC = rv.load()
+NAN_VEC = np.load(rv.NAN_NPZ, allow_pickle=False)
 MODES = ["sync", "overlap", "rowmajor", "double"]
 
 
@@ -44,17 +47,29 @@ def _cases():
         for mode in MODES:
             out.append((g, "uint16", 1, mode))
         out.append((g, "float32", 3, "overlap"))
+        out.append((g, "float32", 1, "sync"))
         out.append((g, "int64", 1, "double"))
         out.append((g, "uint8", 0, "rowmajor"))
+    for g in rv.NAN_GEOMETRIES:
+        out.append(("nan:" + g, "float32", 1, "overlap"))
+        out.append(("nan:" + g, "float64", 1, "sync"))
     return out
+
+
+def _vec(geom):
+    """(fixture, geometry name): 'nan:<geom>' selects the NaN-payload set."""
+    if geom.startswith("nan:"):
+        return NAN_VEC, geom[4:]
+    return VEC, geom
 
 
 CASES = _cases()
 
 
 def _run(tmp_path, geom, dtype, method, mode):
+    vec, geom = _vec(geom)
     g = MAN["geometries"][geom]
-    frames = VEC[f"in/{geom}/{dtype}"]
+    frames = vec[f"in/{geom}/{dtype}"]
     fin, fout = tmp_path / "frames.bin", tmp_path / "out.bin"
     fin.write_bytes(np.ascontiguousarray(frames).tobytes())
     spec = (f"{len(g['dims'])} {rv.NP_DTYPES.index(np.dtype(dtype).type)} {method} "
@@ -80,11 +95,12 @@ def _run(tmp_path, geom, dtype, method, mode):
 @pytest.mark.parametrize("geom,dtype,method,mode", CASES,
                          ids=[f"{g}-{d}-{rv.METHOD_NAMES[m]}-{mo}" for g, d, m, mo in CASES])
 def test_adapter_matches_reference(tmp_path, oracle, geom, dtype, method, mode):
+    got = _run(tmp_path, geom, dtype, method, mode)
+    vec, geom = _vec(geom)
     g = MAN["geometries"][geom]
     dt = np.dtype(dtype)
     name = f"{geom}/{dtype}/{rv.METHOD_NAMES[method]}"
-    ev, out = VEC[f"ev/{name}"], VEC[f"out/{name}"]
-    got = _run(tmp_path, geom, dtype, method, mode)
+    ev, out = vec[f"ev/{name}"], vec[f"out/{name}"]
     assert len(got) == ev.shape[0], f"{len(got)} takes vs {ev.shape[0]}"
     off = 0
     n_tiled = 0
@@ -104,7 +120,7 @@ def test_adapter_matches_reference(tmp_path, oracle, geom, dtype, method, mode):
             tiles, _ = oracle.tile_frame(want.view(dt).reshape(h, w), tr, tc)
             want = tiles.view(np.uint8).reshape(-1)
         assert b.size == want.size, f"{ctx}: {b.size} bytes vs {want.size}"
-        bad = rv.same(b, want, dt, nan_bits=False)
+        bad = rv.same(b, want, dt, nan_bits=True)
         assert bad is None, f"{ctx}: {bad.size} elements differ, first at {bad[0]}"
     if mode in ("overlap", "double"):
         assert n_tiled > 0

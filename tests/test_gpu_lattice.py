@@ -90,16 +90,7 @@ def run_case(aqz, oracle, dims, dtype, method, first, n, seed, max_levels=0, pla
     assert counts == [n] * len(geo)
     for L in range(1, len(geo)):
         got = bufs[L].cpu().numpy()
-        if np.dtype(dtype).kind == "f":
-            # NaN payloads may differ (tests/gpu_util.assert_parity's rule:
-            # NaN positions must match); every other value bit for bit
-            g, w = got.view(dtype), want[L].view(dtype)
-            both_nan = np.isnan(g) & np.isnan(w)
-            g_bits = got.view(f"u{np.dtype(dtype).itemsize}")
-            w_bits = want[L].view(f"u{np.dtype(dtype).itemsize}")
-            bad = np.flatnonzero((g_bits != w_bits) & ~both_nan)
-            assert bad.size == 0, f"level {L}: {bad.size} values differ, first at {bad[0]}"
-        elif not np.array_equal(got, want[L]):
+        if not np.array_equal(got, want[L]):  # bytes: NaN payloads included
             bad = np.flatnonzero(got != want[L])
             raise AssertionError(f"level {L}: {bad.size} bytes differ, first at {bad[0]}")
     ds.close()

@@ -9,9 +9,13 @@ zarr::Downsampler compiled unmodified, tests/golden/make_reference_vectors.py).
   level's frames of every geometry whose levels are all taken after every
   frame.
 
-Integers bit-exact; floats bit-exact on every non-NaN value with NaN
-positions equal (NaN payloads are not compared: refvec.same).  No reference
-code runs here — the fixtures travel, the reference does not.
+Every case is compared byte for byte, floats included: NaN payloads must be
+the ones the reference binary made (x86's first-NaN-operand rule and its
+negative default NaN, restated in ds_kernels.hip's x86_add).  The
+NaN-payload set (reference_nan_vectors.npz: inputs dense in quiet and
+signaling NaNs of both signs and random payloads, and infinities) replays the
+same way.  No reference code runs here — the fixtures travel, the reference
+does not.
 """
 import numpy as np
 import pytest
@@ -22,12 +26,14 @@ from gpu_util import empty_device, from_device, launch_stream, to_device, torch_
 pytestmark = pytest.mark.gpu
 
 MAN, VEC = rv.load()
+NAN_VEC = np.load(rv.NAN_NPZ, allow_pickle=False)
 CASES = rv.cases(MAN)
 IDS = [f"{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in CASES]
+NAN_CASES = rv.nan_cases()
+NAN_IDS = [f"nan-{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in NAN_CASES]
 
 
-@pytest.mark.parametrize("geom,dtype,method", CASES, ids=IDS)
-def test_stream_replays_reference_vectors(aqz, geom, dtype, method):
+def _stream_replay(aqz, vec, geom, dtype, method):
     handles = []
 
     def make(dims, dt, m):
@@ -35,24 +41,38 @@ def test_stream_replays_reference_vectors(aqz, geom, dtype, method):
         handles.append(ds)
         return ds
     try:
-        rv.replay(make, MAN, VEC, geom, dtype, method, nan_bits=False)
+        rv.replay(make, MAN, vec, geom, dtype, method, nan_bits=True)
     finally:
         for ds in handles:
             ds.close()
 
 
-BATCH_CASES = [(g, d, m) for g, d, m in CASES if MAN["geometries"][g]["take"] == "all"]
+@pytest.mark.parametrize("geom,dtype,method", CASES, ids=IDS)
+def test_stream_replays_reference_vectors(aqz, geom, dtype, method):
+    _stream_replay(aqz, VEC, geom, dtype, method)
 
 
-@pytest.mark.parametrize("geom,dtype,method", BATCH_CASES,
-                         ids=[f"{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in BATCH_CASES])
-def test_device_batch_reproduces_reference_levels(aqz, geom, dtype, method):
+@pytest.mark.parametrize("geom,dtype,method", NAN_CASES, ids=NAN_IDS)
+def test_stream_replays_reference_nan_vectors(aqz, geom, dtype, method):
+    _stream_replay(aqz, NAN_VEC, geom, dtype, method)
+
+
+BATCH_CASES = [("main", g, d, m) for g, d, m in CASES
+               if MAN["geometries"][g]["take"] == "all"]
+BATCH_CASES += [("nan", g, d, m) for g, d, m in NAN_CASES
+                if MAN["geometries"][g]["take"] == "all"]
+
+
+@pytest.mark.parametrize("vset,geom,dtype,method", BATCH_CASES,
+                         ids=[f"{v}-{g}-{d}-{rv.METHOD_NAMES[m]}" for v, g, d, m in BATCH_CASES])
+def test_device_batch_reproduces_reference_levels(aqz, vset, geom, dtype, method):
     torch = torch_cuda()
+    vec = VEC if vset == "main" else NAN_VEC
     g = MAN["geometries"][geom]
     dt = np.dtype(dtype)
-    frames = VEC[f"in/{geom}/{dtype}"]
+    frames = vec[f"in/{geom}/{dtype}"]
     name = f"{geom}/{dtype}/{rv.METHOD_NAMES[method]}"
-    ev, out = VEC[f"ev/{name}"], VEC[f"out/{name}"]
+    ev, out = vec[f"ev/{name}"], vec[f"out/{name}"]
     # the reference's frames per level, in emit order
     want = {L: [] for L in range(1, len(g["levels"]))}
     off = 0
@@ -78,5 +98,5 @@ def test_device_batch_reproduces_reference_levels(aqz, geom, dtype, method):
         got = from_device(outs[L], np.uint8, (-1,))[:len(frames_L) * w * h * bpp]
         for k, wb in enumerate(frames_L):
             gb = got[k * w * h * bpp:(k + 1) * w * h * bpp]
-            bad = rv.same(gb, wb, dt, nan_bits=False)
+            bad = rv.same(gb, wb, dt, nan_bits=True)
             assert bad is None, f"{name}: level {L} frame {k}: {bad.size} elements differ"

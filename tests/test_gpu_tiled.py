@@ -119,10 +119,9 @@ def test_tiled_batch_dtypes_methods(aqz, oracle, dtype, method):
             want_t, want_nz = oracle.tile_frame(ref[L - 1], tr, tc)
             t, f = got[L - 1]
             assert_parity(t[k], want_t, f"{np.dtype(dtype).name} m{method} f{k} L{L}")
-            if np.dtype(dtype).kind == "f":  # bit-exact, NaN payloads aside
+            if np.dtype(dtype).kind == "f":  # bit-exact, NaN payloads included
                 ib = np.uint32 if dtype == np.float32 else np.uint64
-                m = ~np.isnan(want_t)
-                assert np.array_equal(t[k][m].view(ib), want_t[m].view(ib))
+                assert np.array_equal(t[k].view(ib), want_t.view(ib))
             assert np.array_equal(f[k], want_nz), f"f{k} L{L} zero scan"
 
 

@@ -60,6 +60,35 @@ def test_oracle_replays_reference_vectors(oracle, geom, dtype, method):
     rv.replay(_oracle_make(oracle), MAN, VEC, geom, dtype, method, nan_bits=True)
 
 
+NAN_VEC = np.load(rv.NAN_NPZ, allow_pickle=False)
+NAN_CASES = rv.nan_cases()
+NAN_IDS = [f"{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in NAN_CASES]
+
+
+def test_nan_fixture_discriminates_payloads():
+    """The NaN-payload set holds what it is for: signaling NaNs among the
+    inputs, and Mean outputs with several distinct NaN bit patterns,
+    including the negative default NaN that x86 makes for inf - inf."""
+    for dname, ut, mant, ebits, dnan in (
+            ("float32", np.uint32, 23, 8, 0xFFC00000),
+            ("float64", np.uint64, 52, 11, 0xFFF8000000000000)):
+        x = NAN_VEC[f"in/xy_odd_37x29/{dname}"].view(ut).reshape(-1)
+        exp = (x >> ut(mant)) & ut((1 << ebits) - 1)
+        frac = x & ut((1 << mant) - 1)
+        is_nan = (exp == ut((1 << ebits) - 1)) & (frac != 0)
+        snan = is_nan & (((x >> ut(mant - 1)) & ut(1)) == 0)
+        assert snan.sum() > 100
+        out = NAN_VEC[f"out/xy_odd_37x29/{dname}/mean"].view(ut)
+        f = out.view(np.float32 if ut is np.uint32 else np.float64)
+        pats = set(out[np.isnan(f)].tolist())
+        assert dnan in pats and len(pats) > 50
+
+
+@pytest.mark.parametrize("geom,dtype,method", NAN_CASES, ids=NAN_IDS)
+def test_oracle_replays_reference_nan_vectors(oracle, geom, dtype, method):
+    rv.replay(_oracle_make(oracle), MAN, NAN_VEC, geom, dtype, method, nan_bits=True)
+
+
 @pytest.mark.parametrize("geom", list(rv.GEOMETRIES))
 def test_planners_equal_reference_levels(oracle, aqz, geom):
     g = MAN["geometries"][geom]
