@@ -52,6 +52,8 @@ EXPORTS = (
     "aqz_shard_unit", "aqz_node_create", "aqz_node_destroy", "aqz_node_handle_count",
     "aqz_node_handle", "aqz_node_run_host_batch", "aqz_node_last_error",
     "aqz_node_add_frame", "aqz_node_take_frame", "aqz_node_flush",
+    "aqz_node_run_device_batch", "aqz_node_wait_input", "aqz_ds_wait_input",
+    "aqz_node_set_level_tiling",
 )
 
 
@@ -215,6 +217,11 @@ def lib() -> ctypes.CDLL:
     L.aqz_node_add_frame.argtypes = [vp, vp, sz]
     L.aqz_node_take_frame.argtypes = [vp, u32, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(i32)]
     L.aqz_node_flush.argtypes = [vp]
+    L.aqz_node_wait_input.argtypes = [vp]
+    L.aqz_node_set_level_tiling.argtypes = [vp, u32, u32, u32]
+    L.aqz_ds_wait_input.argtypes = [vp]
+    L.aqz_node_run_device_batch.argtypes = [vp, vp, i32, u32, ctypes.POINTER(vp),
+                                            ctypes.POINTER(u32), vp, u32]
     _lib = L
     return L
 
@@ -814,3 +821,30 @@ class Node:
         if rc:
             raise AqzError(rc, L.aqz_node_last_error(self._h).decode())
         return list(counts)
+
+    def device_batch_call(self, device_frames: int, src_device: int, n_frames: int,
+                          device_outs, stream: int = 0, stage_all: bool = False):
+        """A prepared aqz_node_run_device_batch: device addresses on
+        `src_device` (device_outs index 0 ignored); the returned callable
+        launches once per call and returns the per-level counts."""
+        n = len(self.geometry)
+        outs = (ctypes.c_void_p * n)(*([None] + [int(p) for p in device_outs[1:]]))
+        counts = (ctypes.c_uint32 * n)()
+        L = lib()
+        fn = L.aqz_node_run_device_batch
+        flags = 1 if stage_all else 0  # AQZ_NODE_STAGE_ALL
+        args = (self._h, ctypes.c_void_p(device_frames), src_device, n_frames, outs, counts,
+                ctypes.c_void_p(stream or None), flags)
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                raise AqzError(rc, L.aqz_node_last_error(self._h).decode())
+            return list(counts)
+        return call
+
+    def run_device_batch(self, device_frames: int, src_device: int, n_frames: int,
+                         device_outs, stream: int = 0, stage_all: bool = False):
+        """aqz_node_run_device_batch (asynchronous on `stream`)."""
+        return self.device_batch_call(device_frames, src_device, n_frames, device_outs,
+                                      stream, stage_all)()

@@ -90,15 +90,15 @@ template<>
 struct float_bits<float>
 {
     using U = uint32_t;
-    static constexpr U quiet = 0x00400000u;
-    static constexpr U default_nan = 0xFFC00000u;
+    static constexpr U quiet() { return 0x00400000u; }
+    static constexpr U default_nan() { return 0xFFC00000u; }
 };
 template<>
 struct float_bits<double>
 {
     using U = uint64_t;
-    static constexpr U quiet = 0x0008000000000000ull;
-    static constexpr U default_nan = 0xFFF8000000000000ull;
+    static constexpr U quiet() { return 0x0008000000000000ull; }
+    static constexpr U default_nan() { return 0xFFF8000000000000ull; }
 };
 
 // x86 `x + y` with its NaN rule (x the first source).
@@ -111,11 +111,11 @@ x86_add(T x, T y)
     const T s = x + y;
     U r;
     if (x != x)
-        r = __builtin_bit_cast(U, x) | FB::quiet;
+        r = __builtin_bit_cast(U, x) | FB::quiet();
     else if (y != y)
-        r = __builtin_bit_cast(U, y) | FB::quiet;
+        r = __builtin_bit_cast(U, y) | FB::quiet();
     else if (s != s)
-        r = FB::default_nan;
+        r = FB::default_nan();
     else
         return s;
     return __builtin_bit_cast(T, r);

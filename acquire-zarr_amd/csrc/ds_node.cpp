@@ -28,6 +28,22 @@
 // background job, so up to D frames (one per handle) are in flight; levels
 // are queued in submission order and handed out in the order one
 // Downsampler emits them.
+//
+// Device-resident batch (aqz_node_run_device_batch, BASELINE config F: frame
+// batches sharded across GPUs over xGMI): the batch and its level outputs
+// live on one GPU.  The same contiguous blocks of whole shard units are
+// dealt; a handle on the batch's own GPU runs its block in place, on the
+// caller's stream; a handle on another GPU pulls its block over xGMI into
+// node-owned staging on its own GPU (hipMemcpyPeerAsync: the GPUs' DMA
+// engines over the point-to-point link, no kernel of ours and no host hop),
+// runs the fused batch there and pushes each level back to the block's place
+// in the outputs.  Each remote block moves in sub-batches through two staging
+// slots on three streams (pull, pyramid, push), so a sub-batch's pull, the
+// previous one's pyramid and the one before's push overlap; every block
+// starts behind an event on the caller's stream and the caller's stream
+// waits for every block's last push, so the call is as asynchronous as
+// aqz_ds_run_device_batch.  One process drives every GPU: no RCCL
+// communicator is involved, and nothing is reduced — the frames only move.
 #include "aqz_downsampler.h"
 #include "abi_guard.hh"
 #include "ds_kernels.hh"
@@ -35,17 +51,39 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
 #include <thread>
 #include <vector>
 
+namespace {
+
+// A handle's staging for device batches whose frames live on another GPU:
+// two slots (input block + every level's output), three streams and the
+// events that order slot reuse across sub-batches and calls.
+struct PeerStage
+{
+    int device = -1;
+    hipStream_t pull = nullptr, run = nullptr, push = nullptr;
+    hipEvent_t pulled[2]{}, ran[2]{}, pushed[2]{}, done = nullptr;
+    uint8_t* stage = nullptr; // 2 slots of slot_bytes
+    size_t slot_bytes = 0;
+    uint32_t next_slot = 0;
+};
+
+} // namespace
+
 struct aqz_node
 {
     std::vector<aqz_ds*> ds;
     std::vector<aqz_level_desc> lv;
     std::vector<size_t> bytes;      // one frame per level
+    // streaming takes per level: (tile_rows, tile_cols), (0, 0) row-major,
+    // and the bytes of one taken frame (tiled: with the zero tile overhang)
+    std::vector<std::pair<uint32_t, uint32_t>> tiling;
+    std::vector<size_t> take_bytes;
     uint32_t unit = 1;              // level-0 frames per shard unit
     std::vector<uint32_t> per_unit; // frames each level emits per unit
     uint64_t frames = 0;            // level-0 frames taken so far (batches and stream)
@@ -65,6 +103,12 @@ struct aqz_node
     std::vector<Add*> in_flight;                      // per handle, or null
     std::vector<std::deque<std::vector<uint8_t>>> ready; // per level, in order
     std::vector<std::vector<uint8_t>> pool;           // spare take buffers
+
+    // Device batches (aqz_node_run_device_batch): per handle, staging used
+    // when the batch lives on another GPU; per source ordinal, the event
+    // that marks the batch ready on the caller's stream.
+    std::vector<PeerStage> peers;
+    std::vector<hipEvent_t> ready_ev;
 };
 
 namespace aqz {
@@ -109,6 +153,105 @@ fail(aqz_node* n, int rc, const std::string& what)
 {
     n->err = what;
     return rc;
+}
+
+// The caller thread's current HIP device is restored on every exit: the
+// handles bind their own ordinals, and a caller driving several GPUs from
+// one thread must not find its later work moved to another one.
+struct DeviceGuard
+{
+    int saved = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&saved) != hipSuccess)
+            saved = -1;
+    }
+    ~DeviceGuard()
+    {
+        if (saved >= 0)
+            (void)hipSetDevice(saved);
+    }
+};
+
+int
+hip_fail(aqz_node* n, hipError_t e, const std::string& what)
+{
+    return fail(n, e == hipErrorOutOfMemory ? AQZ_OUT_OF_MEMORY : AQZ_INTERNAL_ERROR,
+                what + ": " + hipGetErrorString(e));
+}
+
+void
+release_peer(PeerStage& p)
+{
+    if (p.device < 0)
+        return;
+    (void)hipSetDevice(p.device);
+    for (hipStream_t s : { p.pull, p.run, p.push })
+        if (s)
+            (void)hipStreamSynchronize(s);
+    for (int k = 0; k < 2; ++k)
+        for (hipEvent_t e : { p.pulled[k], p.ran[k], p.pushed[k] })
+            if (e)
+                (void)hipEventDestroy(e);
+    if (p.done)
+        (void)hipEventDestroy(p.done);
+    for (hipStream_t s : { p.pull, p.run, p.push })
+        if (s)
+            (void)hipStreamDestroy(s);
+    if (p.stage)
+        (void)hipFree(p.stage);
+    p = PeerStage{};
+}
+
+// Staging of handle h on its device, with two slots of at least `slot`
+// bytes (grown, never shrunk; growth waits for the slots' last use).
+int
+peer_stage(aqz_node* n, uint32_t h, int src_device, size_t slot)
+{
+    PeerStage& p = n->peers[h];
+    const int dev = aqz_ds_device(n->ds[h]);
+    hipError_t e = hipSetDevice(dev);
+    if (e != hipSuccess)
+        return hip_fail(n, e, "node device batch: hipSetDevice");
+    if (p.device < 0) {
+        p.device = dev;
+        for (hipStream_t* s : { &p.pull, &p.run, &p.push })
+            if ((e = hipStreamCreateWithFlags(s, hipStreamNonBlocking)) != hipSuccess)
+                return hip_fail(n, e, "node device batch: stream");
+        for (int k = 0; k < 2; ++k)
+            for (hipEvent_t* ev : { &p.pulled[k], &p.ran[k], &p.pushed[k] })
+                if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+                    return hip_fail(n, e, "node device batch: event");
+        if ((e = hipEventCreateWithFlags(&p.done, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(n, e, "node device batch: event");
+        // direct xGMI access to the batch's GPU where the pair has it (the
+        // copies work either way; this keeps them off any host bounce)
+        int can = 0;
+        if (dev != src_device && hipDeviceCanAccessPeer(&can, dev, src_device) == hipSuccess &&
+            can) {
+            e = hipDeviceEnablePeerAccess(src_device, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                return hip_fail(n, e, "node device batch: peer access");
+            (void)hipGetLastError(); // clear "already enabled"
+        }
+    }
+    if (p.slot_bytes < slot) {
+        for (hipStream_t s : { p.pull, p.run, p.push })
+            if ((e = hipStreamSynchronize(s)) != hipSuccess)
+                return hip_fail(n, e, "node device batch: drain before growing staging");
+        if (p.stage)
+            (void)hipFree(p.stage);
+        p.stage = nullptr;
+        p.slot_bytes = 0;
+        void* mem = nullptr;
+        if ((e = hipMalloc(&mem, 2 * slot)) != hipSuccess)
+            return hip_fail(n, e,
+                            "node device batch: staging of " + std::to_string(2 * slot) +
+                              " bytes on device " + std::to_string(dev));
+        p.stage = static_cast<uint8_t*>(mem);
+        p.slot_bytes = slot;
+    }
+    return AQZ_OK;
 }
 
 // Wait for handle h's add in flight; its takes become publishable.
@@ -272,6 +415,7 @@ aqz_node_create(const aqz_level_desc* levels,
         if (levels && n_levels > 0 && n_levels <= AQZ_MAX_LEVELS)
             if (int rc = aqz_shard_unit(levels, n_levels, &unit, per_unit.data()))
                 return rc;
+        DeviceGuard guard;
         auto* n = new aqz_node();
         for (uint32_t d = 0; d < n_devices; ++d) {
             aqz_ds* h = nullptr;
@@ -285,10 +429,13 @@ aqz_node_create(const aqz_level_desc* levels,
         n->lv.assign(levels, levels + n_levels);
         for (uint32_t L = 0; L < n_levels; ++L)
             n->bytes.push_back(aqz_ds_level_bytes(n->ds[0], L));
+        n->tiling.assign(n_levels, { 0u, 0u });
+        n->take_bytes = n->bytes;
         n->unit = unit;
         n->per_unit = per_unit;
         n->in_flight.assign(n_devices, nullptr);
         n->ready.resize(n_levels);
+        n->peers.resize(n_devices);
         *out = n;
         return AQZ_OK;
     } catch (...) {
@@ -301,6 +448,15 @@ aqz_node_destroy(aqz_node* n)
 {
     if (!n)
         return;
+    DeviceGuard guard;
+    // staging drains its streams before it is freed
+    for (PeerStage& p : n->peers)
+        release_peer(p);
+    for (size_t d = 0; d < n->ready_ev.size(); ++d)
+        if (n->ready_ev[d]) {
+            (void)hipSetDevice(int(d));
+            (void)hipEventDestroy(n->ready_ev[d]);
+        }
     // aqz_ds_destroy settles a handle's add in flight before freeing it, so
     // no background take still writes into this node's buffers
     for (aqz_ds* h : n->ds)
@@ -314,6 +470,7 @@ aqz_node_add_frame(aqz_node* n, const void* host_frame, size_t nbytes)
     try {
         if (!n)
             return AQZ_INVALID_ARGUMENT;
+        DeviceGuard guard;
         if (!host_frame || nbytes != n->bytes[0])
             return fail(n, AQZ_INVALID_ARGUMENT,
                         "node_add_frame: frame of " + std::to_string(nbytes) + " bytes, expected " +
@@ -337,8 +494,10 @@ aqz_node_add_frame(aqz_node* n, const void* host_frame, size_t nbytes)
                 b = std::move(n->pool.back());
                 n->pool.pop_back();
             }
-            b.resize(n->bytes[L]);
+            b.resize(n->take_bytes[L]);
             a.takes[L].mode = AQZ_TAKE_INTO;
+            a.takes[L].tile_rows = n->tiling[L].first;
+            a.takes[L].tile_cols = n->tiling[L].second;
             a.takes[L].dst = b.data();
             a.takes[L].cap = b.size();
         }
@@ -371,6 +530,7 @@ aqz_node_take_frame(aqz_node* n,
             *nbytes = 0;
         if (level == 0 || level >= n->lv.size())
             return AQZ_OK;
+        DeviceGuard guard;
         if (int rc = settle_finished(n))
             return rc;
         publish(n);
@@ -399,7 +559,53 @@ aqz_node_flush(aqz_node* n)
     try {
         if (!n)
             return AQZ_INVALID_ARGUMENT;
+        DeviceGuard guard;
         return flush_all(n);
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+int
+aqz_node_set_level_tiling(aqz_node* n, uint32_t level, uint32_t tile_rows, uint32_t tile_cols)
+{
+    try {
+        if (!n)
+            return AQZ_INVALID_ARGUMENT;
+        if (level == 0 || level >= n->lv.size() || (tile_rows == 0) != (tile_cols == 0))
+            return fail(n, AQZ_INVALID_ARGUMENT, "node_set_level_tiling: bad level or tile shape");
+        if (n->frames != 0)
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_set_level_tiling: frames were already added");
+        DeviceGuard guard;
+        // every handle tiles the level on its GPU right behind the pyramid
+        for (aqz_ds* h : n->ds)
+            if (int rc = aqz_ds_set_level_tiling(h, level, tile_rows, tile_cols))
+                return fail(n, rc, std::string("node_set_level_tiling: ") + aqz_ds_last_error(h));
+        n->tiling[level] = { tile_rows, tile_cols };
+        const aqz_level_desc& d = n->lv[level];
+        n->take_bytes[level] =
+          tile_rows == 0 ? n->bytes[level]
+                         : size_t((d.width + tile_cols - 1) / tile_cols) *
+                             ((d.height + tile_rows - 1) / tile_rows) * tile_rows * tile_cols *
+                             (n->bytes[level] / (size_t(d.width) * d.height));
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+int
+aqz_node_wait_input(aqz_node* n)
+{
+    try {
+        if (!n)
+            return AQZ_INVALID_ARGUMENT;
+        for (uint32_t h = 0; h < n->ds.size(); ++h)
+            if (n->in_flight[h])
+                if (int rc = aqz_ds_wait_input(n->ds[h]))
+                    return fail(n, rc, "node_wait_input: handle " + std::to_string(h));
+        return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(n);
     }
@@ -427,6 +633,7 @@ aqz_node_run_host_batch(aqz_node* n,
     try {
         if (!n)
             return AQZ_INVALID_ARGUMENT;
+        DeviceGuard guard;
         const uint32_t nl = uint32_t(n->lv.size());
         if (!host_frames || !host_out_levels)
             return fail(n, AQZ_INVALID_ARGUMENT, "node_run_host_batch: null buffer");
@@ -497,6 +704,185 @@ aqz_node_run_host_batch(aqz_node* n,
                                 "node_run_host_batch: handle " + std::to_string(d) +
                                   " emitted an unexpected frame count at level " +
                                   std::to_string(L));
+        if (out_counts) {
+            out_counts[0] = n_frames;
+            for (uint32_t L = 1; L < nl; ++L)
+                out_counts[L] = units * n->per_unit[L];
+        }
+        n->frames += n_frames;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+int
+aqz_node_run_device_batch(aqz_node* n,
+                          const void* device_frames,
+                          int src_device,
+                          uint32_t n_frames,
+                          void* const* device_out_levels,
+                          uint32_t* out_counts,
+                          void* hip_stream,
+                          uint32_t flags)
+{
+    try {
+        if (!n)
+            return AQZ_INVALID_ARGUMENT;
+        DeviceGuard guard;
+        const uint32_t nl = uint32_t(n->lv.size());
+        if (!device_frames || !device_out_levels)
+            return fail(n, AQZ_INVALID_ARGUMENT, "node_run_device_batch: null buffer");
+        for (uint32_t L = 1; L < nl; ++L)
+            if (!device_out_levels[L])
+                return fail(n, AQZ_INVALID_ARGUMENT,
+                            "node_run_device_batch: null output for level " + std::to_string(L));
+        if (flags & ~uint32_t(AQZ_NODE_STAGE_ALL))
+            return fail(n, AQZ_INVALID_ARGUMENT, "node_run_device_batch: unknown flags");
+        int n_dev = 0;
+        if (hipGetDeviceCount(&n_dev) != hipSuccess || src_device < 0 || src_device >= n_dev)
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_run_device_batch: no HIP device " + std::to_string(src_device));
+        if (n->frames % n->unit != 0)
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_run_device_batch: the stream stands inside a shard unit (" +
+                          std::to_string(n->frames % n->unit) + " of " +
+                          std::to_string(n->unit) + " frames)");
+        if (n_frames % n->unit != 0)
+            return fail(n, AQZ_INVALID_ARGUMENT,
+                        "node_run_device_batch: " + std::to_string(n_frames) +
+                          " frames is not a whole number of shard units of " +
+                          std::to_string(n->unit) + " (Z pairs must stay on one GPU)");
+        if (int rc = flush_all(n))
+            return rc;
+        const uint32_t units = n_frames / n->unit;
+        const uint32_t D = uint32_t(n->ds.size());
+        std::vector<uint32_t> first(D + 1, 0);
+        for (uint32_t d = 0; d < D; ++d)
+            first[d + 1] = first[d] + units / D + (d < units % D ? 1 : 0);
+
+        // bytes of one shard unit: its input frames, and each level's output
+        size_t unit_out = 0;
+        std::vector<size_t> unit_bytes(nl, 0);
+        unit_bytes[0] = size_t(n->unit) * n->bytes[0];
+        for (uint32_t L = 1; L < nl; ++L) {
+            unit_bytes[L] = size_t(n->per_unit[L]) * n->bytes[L];
+            unit_out += unit_bytes[L];
+        }
+        // sub-batch of a remote block: the units that fit the staging budget
+        // ($AQZ_NODE_STAGE_MB per slot, default 256 MiB), at least one
+        size_t budget = size_t(256) << 20;
+        if (const char* env = std::getenv("AQZ_NODE_STAGE_MB"))
+            if (long v = std::atol(env); v > 0)
+                budget = size_t(v) << 20;
+        const uint32_t sub_units =
+          uint32_t(std::max<size_t>(1, budget / (unit_bytes[0] + unit_out)));
+
+        hipError_t e = hipSetDevice(src_device);
+        if (e != hipSuccess)
+            return hip_fail(n, e, "node_run_device_batch: hipSetDevice");
+        hipStream_t caller = static_cast<hipStream_t>(hip_stream);
+        if (n->ready_ev.size() < size_t(n_dev))
+            n->ready_ev.resize(n_dev, nullptr);
+        hipEvent_t& ready = n->ready_ev[src_device];
+        if (!ready && (e = hipEventCreateWithFlags(&ready, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(n, e, "node_run_device_batch: event");
+        if ((e = hipEventRecord(ready, caller)) != hipSuccess)
+            return hip_fail(n, e, "node_run_device_batch: event record");
+
+        const uint8_t* in = static_cast<const uint8_t*>(device_frames);
+        std::vector<hipEvent_t> joins;
+        int rc = AQZ_OK;
+        for (uint32_t d = 0; d < D && rc == AQZ_OK; ++d) {
+            const uint32_t u0 = first[d], nu = first[d + 1] - first[d];
+            if (nu == 0)
+                continue;
+            aqz_ds* h = n->ds[d];
+            const int dev = aqz_ds_device(h);
+            std::vector<void*> outs(nl, nullptr);
+            for (uint32_t L = 1; L < nl; ++L)
+                outs[L] = static_cast<uint8_t*>(device_out_levels[L]) + size_t(u0) * unit_bytes[L];
+            std::vector<uint32_t> cnt(nl, 0);
+            if (dev == src_device && !(flags & AQZ_NODE_STAGE_ALL)) {
+                // in place, on the caller's stream
+                rc = aqz_ds_run_device_batch(h, in + size_t(u0) * unit_bytes[0], nu * n->unit,
+                                             outs.data(), cnt.data(), caller);
+                if (rc)
+                    return fail(n, rc, "node_run_device_batch: handle " + std::to_string(d) +
+                                         ": " + aqz_ds_last_error(h));
+                for (uint32_t L = 1; L < nl; ++L)
+                    if (cnt[L] != nu * n->per_unit[L])
+                        return fail(n, AQZ_INTERNAL_ERROR,
+                                    "node_run_device_batch: handle " + std::to_string(d) +
+                                      " emitted an unexpected frame count at level " +
+                                      std::to_string(L));
+                continue;
+            }
+            const uint32_t g_max = std::min(sub_units, nu);
+            if ((rc = peer_stage(n, d, src_device, size_t(g_max) * (unit_bytes[0] + unit_out))))
+                break;
+            PeerStage& p = n->peers[d];
+            if ((e = hipStreamWaitEvent(p.pull, ready, 0)) != hipSuccess)
+                return hip_fail(n, e, "node_run_device_batch: wait for the batch");
+            for (uint32_t j = 0; j < nu; j += g_max) {
+                const uint32_t g = std::min(g_max, nu - j);
+                const uint32_t s = p.next_slot;
+                p.next_slot ^= 1u;
+                uint8_t* slot = p.stage + size_t(s) * p.slot_bytes;
+                std::vector<void*> souts(nl, nullptr);
+                size_t off = size_t(g) * unit_bytes[0];
+                for (uint32_t L = 1; L < nl; ++L) {
+                    souts[L] = slot + off;
+                    off += size_t(g) * unit_bytes[L];
+                }
+                // pull: once the slot's previous pyramid has read its input
+                if ((e = hipStreamWaitEvent(p.pull, p.ran[s], 0)) != hipSuccess ||
+                    (e = hipMemcpyPeerAsync(slot, dev, in + size_t(u0 + j) * unit_bytes[0],
+                                            src_device, size_t(g) * unit_bytes[0], p.pull)) !=
+                      hipSuccess ||
+                    (e = hipEventRecord(p.pulled[s], p.pull)) != hipSuccess)
+                    return hip_fail(n, e, "node_run_device_batch: pull over xGMI");
+                // pyramid: once pulled and the slot's previous push has left
+                if ((e = hipStreamWaitEvent(p.run, p.pulled[s], 0)) != hipSuccess ||
+                    (e = hipStreamWaitEvent(p.run, p.pushed[s], 0)) != hipSuccess)
+                    return hip_fail(n, e, "node_run_device_batch: stream order");
+                rc = aqz_ds_run_device_batch(h, slot, g * n->unit, souts.data(), cnt.data(),
+                                             p.run);
+                if (rc)
+                    return fail(n, rc, "node_run_device_batch: handle " + std::to_string(d) +
+                                         ": " + aqz_ds_last_error(h));
+                for (uint32_t L = 1; L < nl; ++L)
+                    if (cnt[L] != g * n->per_unit[L])
+                        return fail(n, AQZ_INTERNAL_ERROR,
+                                    "node_run_device_batch: handle " + std::to_string(d) +
+                                      " emitted an unexpected frame count at level " +
+                                      std::to_string(L));
+                if ((e = hipSetDevice(dev)) != hipSuccess ||
+                    (e = hipEventRecord(p.ran[s], p.run)) != hipSuccess ||
+                    (e = hipStreamWaitEvent(p.push, p.ran[s], 0)) != hipSuccess)
+                    return hip_fail(n, e, "node_run_device_batch: stream order");
+                // push: each level to the block's place in the outputs
+                for (uint32_t L = 1; L < nl; ++L)
+                    if ((e = hipMemcpyPeerAsync(static_cast<uint8_t*>(outs[L]) +
+                                                  size_t(j) * unit_bytes[L],
+                                                src_device, souts[L], dev,
+                                                size_t(g) * unit_bytes[L], p.push)) != hipSuccess)
+                        return hip_fail(n, e, "node_run_device_batch: push over xGMI");
+                if ((e = hipEventRecord(p.pushed[s], p.push)) != hipSuccess)
+                    return hip_fail(n, e, "node_run_device_batch: event record");
+            }
+            if ((e = hipEventRecord(p.done, p.push)) != hipSuccess)
+                return hip_fail(n, e, "node_run_device_batch: event record");
+            joins.push_back(p.done);
+        }
+        if (rc)
+            return rc;
+        // the caller's stream owns the outputs again once every push is done
+        if ((e = hipSetDevice(src_device)) != hipSuccess)
+            return hip_fail(n, e, "node_run_device_batch: hipSetDevice");
+        for (hipEvent_t ev : joins)
+            if ((e = hipStreamWaitEvent(caller, ev, 0)) != hipSuccess)
+                return hip_fail(n, e, "node_run_device_batch: join");
         if (out_counts) {
             out_counts[0] = n_frames;
             for (uint32_t L = 1; L < nl; ++L)

@@ -204,6 +204,9 @@ struct aqz_ds
         std::mutex m;
         std::condition_variable cv;
         const void* frame = nullptr; // the pending job's frame, null when idle
+        // the pending job's frame while the job may still read it (until its
+        // upload is done); null once the caller may reuse it
+        const void* input = nullptr;
         aqz_level_take* takes = nullptr; // aqz_ds_add_frame_async_take's takes
         bool stop = false;
         int rc = 0;                  // status of the last finished job
@@ -812,6 +815,13 @@ async_worker(aqz_ds* ds)
         int rc;
         try {
             rc = add_host_frame(ds, frame);
+            // add_host_frame returns once the upload no longer reads the
+            // caller's frame (or on failure): release it before the takes
+            {
+                std::lock_guard<std::mutex> in(a.m);
+                a.input = nullptr;
+            }
+            a.cv.notify_all();
             if (rc == AQZ_OK && takes)
                 rc = run_takes(ds, takes);
         } catch (...) {
@@ -820,6 +830,7 @@ async_worker(aqz_ds* ds)
         lk.lock();
         a.rc = rc;
         a.frame = nullptr;
+        a.input = nullptr;
         a.takes = nullptr;
         a.cv.notify_all();
     }
@@ -1265,6 +1276,7 @@ aqz_ds_add_frame_async(aqz_ds* ds, const void* host_frame, size_t nbytes)
         {
             std::lock_guard<std::mutex> lk(a.m);
             a.frame = host_frame;
+            a.input = host_frame;
         }
         a.cv.notify_all();
         return AQZ_OK;
@@ -1316,6 +1328,7 @@ aqz_ds_add_frame_async_take(aqz_ds* ds,
         {
             std::lock_guard<std::mutex> lk(a.m);
             a.frame = host_frame;
+            a.input = host_frame;
             a.takes = takes;
         }
         a.cv.notify_all();
@@ -1332,6 +1345,23 @@ aqz_ds_wait(aqz_ds* ds)
         if (!ds)
             return AQZ_INVALID_ARGUMENT;
         return settle(ds);
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
+}
+
+int
+aqz_ds_wait_input(aqz_ds* ds)
+{
+    try {
+        if (!ds)
+            return AQZ_INVALID_ARGUMENT;
+        auto& a = ds->async;
+        if (!a.worker.joinable())
+            return AQZ_OK;
+        std::unique_lock<std::mutex> lk(a.m);
+        a.cv.wait(lk, [&] { return a.input == nullptr; });
+        return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(ds);
     }

@@ -228,13 +228,26 @@ def parse(argv=None):
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE traffic passes")
     p.add_argument("--sink", default="",
-                   help="directory: also time the streaming path with every level "
-                        "frame written to a per-level raw file by a writer thread "
-                        "(BASELINE config C2's filesystem sink)")
+                   help="directory for the filesystem-sink legs (default: a temporary "
+                        "directory): BASELINE config C2 (2048^2 u16, 4 levels) always, "
+                        "and with --sink also the workload itself; raw level files, "
+                        "fsync'd")
     p.add_argument("--xgmi-scatter", action="store_true",
-                   help="N>1 only (BASELINE config F): every step, rank 0 scatters "
-                        "the ranks' frames over xGMI with RCCL p2p and gathers "
-                        "the levels back; timed end to end")
+                   help="BASELINE config F through the library: every step, rank 0's "
+                        "batch of (GPUs x B) frames is sharded over the node's GPUs by "
+                        "aqz_node_run_device_batch (peer copies over xGMI, levels back "
+                        "in frame order); rank 0 drives every GPU, the other ranks "
+                        "wait; timed end to end")
+    p.add_argument("--node-devices", default="",
+                   help="--xgmi-scatter: HIP ordinals of the node's handles (default: "
+                        "one per rank); repeat one to rehearse on a smaller box, "
+                        "e.g. 0,0")
+    p.add_argument("--stage-all", action="store_true",
+                   help="--xgmi-scatter: every block takes the remote-GPU staging path, "
+                        "also on the batch's own GPU (AQZ_NODE_STAGE_ALL)")
+    p.add_argument("--xgmi-rccl", action="store_true",
+                   help="N>1 only: the same scatter/gather as torch.distributed RCCL "
+                        "p2p between the rank processes instead (one rank per GPU)")
     p.add_argument("--tiled", action="store_true",
                    help="emit every level chunk-tiled (chunk x chunk tiles) from the "
                         "pyramid kernel itself: aqz_ds_run_device_batch_tiled "
@@ -338,7 +351,29 @@ def main():
     assert sptr, "need a non-null HIP stream"
 
     counts = [0] * n_levels
-    xgmi = args.xgmi_scatter and dist is not None
+    xgmi = args.xgmi_rccl and dist is not None
+    # --xgmi-scatter: the library's node over the node's GPUs, from rank 0
+    node_devices = None
+    if args.xgmi_scatter:
+        node_devices = ([int(x) for x in args.node_devices.split(",")] if args.node_devices
+                        else list(range(world)))
+        if len(node_devices) < 2:
+            raise SystemExit("--xgmi-scatter: needs two or more GPUs (ranks or --node-devices)")
+    xnode = None
+    if node_devices is not None and rank == 0:
+        ND = len(node_devices)
+        pool = torch.empty(ND * B * frame_bytes, dtype=torch.uint8, device="cuda")
+        for r in range(ND):
+            pool[r * B * frame_bytes:(r + 1) * B * frame_bytes].copy_(d_in)
+        pool_levels = [None] + [torch.empty(ND * o.numel(), dtype=torch.uint8, device="cuda")
+                                for o in outs[1:]]
+        torch.cuda.synchronize()
+        node = aqz.Node(geo, dtype, method, node_devices)
+        xnode = {"node": node, "pool": pool, "levels": pool_levels, "n": ND,
+                 "call": node.device_batch_call(pool.data_ptr(), device, ND * B,
+                                                [0] + [t.data_ptr() for t in pool_levels[1:]],
+                                                sptr, stage_all=args.stage_all),
+                 "counts": None}
     if xgmi:
         # config F: rank 0's pool holds every rank's frames; levels return
         # to rank 0.  Rank 0 computes on the first block of its pool.
@@ -362,10 +397,18 @@ def main():
 
     def step(ev=None):
         """One step; `ev` = (start, kernel_start, kernel_end, end) events
-        recorded on the launch stream, so that in --xgmi-scatter mode the
+        recorded on the launch stream, so that in --xgmi-rccl mode the
         kernel's own time is separate from the p2p scatter/gather around it
         (the p2p work is joined onto `stream` by wait())."""
-        if xgmi:
+        if node_devices is not None:
+            # the whole node's batch from rank 0 (the other ranks idle)
+            if xnode is not None:
+                if ev:
+                    ev[1].record(stream)
+                xnode["counts"] = xnode["call"]()
+                if ev:
+                    ev[2].record(stream)
+        elif xgmi:
             if ev:
                 ev[0].record(stream)
             mine = scatter_frames(pool, d_in, frame_bytes, B, dist, rank, world)
@@ -422,6 +465,12 @@ def main():
                     if not args.no_flags:
                         gf = flags[L][k * len(nz) * S:(k + 1) * len(nz) * S].cpu().numpy()
                         ok = ok and np.array_equal(gf.reshape(len(nz), S).any(axis=1), nz)
+                elif xnode is not None:
+                    # the last block: it went through the last handle's GPU
+                    fb = w * h * bpp
+                    base = (xnode["n"] - 1) * outs[L].numel()
+                    got = xnode["levels"][L][base + k * fb:base + (k + 1) * fb].cpu().numpy()
+                    ok = ok and np.array_equal(got, r.view(np.uint8).reshape(-1))
                 else:
                     got = outs[L][k * w * h * bpp:(k + 1) * w * h * bpp].cpu().numpy()
                     ok = ok and np.array_equal(got, r.view(np.uint8).reshape(-1))
@@ -454,8 +503,41 @@ def main():
             evs[0][2].record(stream)
 
     elapsed = timed_region(timed_step, args.steps, dist, torch.cuda.synchronize)
-    launch_ms = ([e[1].elapsed_time(e[2]) for e in evs] if per_launch else
-                 [evs[0][1].elapsed_time(evs[0][2]) / args.steps])
+    xgmi_node = None
+    if node_devices is not None:
+        # the node's span per step (rank 0), then the kernel alone: the
+        # plain local batch back to back, as in the N=1 line
+        if xnode is not None:
+            span_ms = evs[0][1].elapsed_time(evs[0][2]) / args.steps
+            ND = xnode["n"]
+            remote = sum(1 for d in node_devices if d != device) if not args.stage_all else ND
+            # per remote block: its frames pulled, its levels pushed back
+            moved = remote * sum(o.numel() for o in [d_in] + outs[1:])
+            xgmi_node = {"ms_per_step": round(span_ms, 4), "devices": node_devices,
+                         "frames_per_step": ND * B,
+                         "bytes_moved_per_step": moved,
+                         "moved_GBps": round(moved / (span_ms * 1e-3) / 1e9, 1),
+                         "staged_blocks": remote,
+                         "counts": xnode["counts"],
+                         "path": "aqz_node_run_device_batch: rank 0's batch dealt in whole "
+                                 "shard units, remote blocks pulled/pushed by hipMemcpyPeerAsync "
+                                 "(xGMI DMA) through two staging slots per GPU, levels back "
+                                 "in frame order"}
+            if len(set(node_devices)) < len(node_devices):
+                xgmi_node["rehearsal"] = (f"{len(node_devices)} handles on "
+                                          f"{len(set(node_devices))} device(s): the staged "
+                                          "copies stay on one GPU")
+        kev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda.synchronize()
+        kev[0].record(stream)
+        for _ in range(args.steps):
+            counts[:] = batch()
+        kev[1].record(stream)
+        torch.cuda.synchronize()
+        launch_ms = [kev[0].elapsed_time(kev[1]) / args.steps]
+    else:
+        launch_ms = ([e[1].elapsed_time(e[2]) for e in evs] if per_launch else
+                     [evs[0][1].elapsed_time(evs[0][2]) / args.steps])
     comm_ms = ([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3]) for e in evs]
                if xgmi else None)
     dev = "cuda" if (dist is not None and dist.get_backend() == "nccl") else "cpu"
@@ -475,7 +557,8 @@ def main():
             rank_comm_ms = [float(x) for x in t[world:].cpu()]
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = aggregate_gpix(world, B, W, H, args.steps, elapsed)
+    value = aggregate_gpix(len(node_devices) if node_devices else world, B, W, H, args.steps,
+                           elapsed)
 
     read_bytes, alg_bytes = algorithmic_bytes(geo, counts, B, args.method, bpp,
                                               tile=(chunk, chunk) if args.tiled else None)
@@ -541,10 +624,22 @@ def main():
                                                          dtype, chunk)
             # §8(f) row 3 end to end: c-blosc frames of device chunks vs c-blosc
             e2e["blosc_frames"] = measure_blosc_frames(aqz, torch)
+            # BASELINE configs[1]: 2048^2 uint16, 4 levels, filesystem sink
+            # (in a temporary directory, or under --sink)
+            import tempfile
+            c2_dims = [(aqz.TIME, 0, 1, 1), (aqz.SPACE, 2048, 256, 1), (aqz.SPACE, 2048, 256, 1)]
+            c2_geo = aqz.level_geometry(aqz.plan_levels(c2_dims))
+            sink_root = args.sink or None
+            if sink_root:
+                os.makedirs(sink_root, exist_ok=True)
+            with tempfile.TemporaryDirectory(dir=sink_root) as tmp:
+                e2e["c2_filesystem_sink"] = measure_e2e_sink(
+                    aqz, c2_geo, np.uint16, method, args.e2e_frames, device,
+                    os.path.join(tmp, "c2"))
             if args.sink:
                 e2e["filesystem_sink"] = measure_e2e_sink(aqz, geo, dtype, method,
                                                           args.e2e_frames, device,
-                                                          args.sink)
+                                                          os.path.join(args.sink, "w"))
 
     if world > 1 and args.e2e_frames > 0:
         # host-to-host on every GPU at once: each rank over its own PCIe link
@@ -604,17 +699,29 @@ def main():
                                       4: "fused cascade, chunk-tiled levels"}.get(kind, "?"),
                        "parallelism": (f"rank-0 batch scattered/gathered over xGMI "
                                        f"(RCCL p2p) x{world}" if xgmi else
+                                       f"rank-0 batch of {len(node_devices)}x{B} frames sharded "
+                                       f"over devices {node_devices} by aqz_node_run_device_batch"
+                                       if node_devices else
                                        f"frame-sharded x{world}, no collective")
                                       + (f"; process group {dist.get_backend()} "
                                          f"world_size={dist.get_world_size()}"
                                          if dist is not None else ""),
                        "check": check},
             "comm_ms_per_step": (round(max(rank_comm_ms), 4) if xgmi else None),
+            "xgmi_node": xgmi_node,
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
             "e2e": e2e,
         }
+        n_vis = torch.cuda.device_count()
+        if world > 1 and n_vis < world:
+            # ranks share GPUs (a gloo rehearsal on a smaller box): not a
+            # world-GPU result, whatever n_gpus says
+            line["rehearsal"] = (f"{world} ranks on {n_vis} visible device(s): "
+                                 f"not a {world}-GPU measurement")
         print(json.dumps(line), flush=True)
+    if xnode is not None:
+        xnode["node"].close()
     ds.close()
     if dist:
         dist.destroy_process_group()
@@ -1180,13 +1287,31 @@ def measure_async_overlap(ds, geo, frames, n_frames, tile):
                     "take_frame_tiled(every level)"}
 
 
+def _fs_type(path):
+    """Filesystem type holding `path` (the longest /proc/mounts prefix)."""
+    best, kind = "", "?"
+    try:
+        real = os.path.realpath(path)
+        with open("/proc/mounts") as f:
+            for line in f:
+                parts = line.split()
+                mnt = parts[1]
+                if (real == mnt or real.startswith(mnt.rstrip("/") + "/")) and len(mnt) > len(best):
+                    best, kind = mnt, parts[2]
+    except OSError:
+        pass
+    return kind
+
+
 def measure_e2e_sink(aqz, geo, dtype, method, n_frames, device, sink_dir):
-    """Streaming drop-in path into a filesystem sink: add_frame + take_frame
-    of every level, each level frame handed to a writer thread that appends
-    it to <sink_dir>/level_<L>.raw (the reference's sink writes on pool
-    threads, array.cpp:664-811).  Timed to the last byte written and fsync'd.
-    Raw level buffers stand in for Zarr chunks: the full acquire-zarr library
-    (blosc, crc32c, minio-cpp, nlohmann) cannot be built here."""
+    """Streaming drop-in path into a filesystem sink (BASELINE configs[1]'s
+    "filesystem sink"): per frame add_frame + take_frame of every level, the
+    frame itself and each level frame handed to writer threads that append
+    them to <sink_dir>/level_<L>.raw (the reference's sink writes on pool
+    threads, array.cpp:664-811).  Timed to the last byte written and
+    fsync'd.  Raw level files stand in for the Zarr store: no chunking,
+    compression or metadata — the acquire-zarr library around the
+    downsampler (minio-cpp, crc32c) cannot be built here."""
     import concurrent.futures as cf
     import shutil
     W, H, _ = geo[0]
@@ -1198,32 +1323,47 @@ def measure_e2e_sink(aqz, geo, dtype, method, n_frames, device, sink_dir):
         frames = [rng.integers(0, np.iinfo(dtype).max, (H, W), dtype=dtype,
                                endpoint=True) for _ in range(4)]
     files = {L: open(os.path.join(sink_dir, f"level_{L}.raw"), "wb")
-             for L in range(1, len(geo))}
+             for L in range(len(geo))}
     ds = aqz.Downsampler(geo, dtype, method, device=device)
+    for i in range(2):  # warm: allocations, first launches
+        ds.add_frame(frames[i])
+        for L in range(1, len(geo)):
+            ds.take_frame(L)
     written = 0
-    with cf.ThreadPoolExecutor(max_workers=2) as pool:
-        futs = []
-        t0 = time.perf_counter()
-        for i in range(n_frames):
-            ds.add_frame(frames[i % 4])
-            for L in range(1, len(geo)):
-                f = ds.take_frame(L)
-                if f is not None:
-                    futs.append(pool.submit(files[L].write, f.tobytes()))
-                    written += f.nbytes
-        for fu in futs:
-            fu.result()
-        for fh in files.values():
-            fh.flush()
-            os.fsync(fh.fileno())
-        el = time.perf_counter() - t0
+    # one writer thread per level file: each file's frames land in order
+    pools = {L: cf.ThreadPoolExecutor(max_workers=1) for L in files}
+    futs = []
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        f0 = frames[i % 4]
+        ds.add_frame(f0)
+        futs.append(pools[0].submit(files[0].write, f0))
+        written += f0.nbytes
+        for L in range(1, len(geo)):
+            f = ds.take_frame(L)
+            if f is not None:
+                futs.append(pools[L].submit(files[L].write, f))
+                written += f.nbytes
+    for fu in futs:
+        fu.result()
+    for fh in files.values():
+        fh.flush()
+        os.fsync(fh.fileno())
+    el = time.perf_counter() - t0
+    for p in pools.values():
+        p.shutdown()
     for fh in files.values():
         fh.close()
     ds.close()
+    fs = _fs_type(sink_dir)
     shutil.rmtree(sink_dir, ignore_errors=True)
     return {"value": round(n_frames * W * H / el / 1e9, 3), "unit": "GPixels/s",
-            "ms_per_frame": round(el / n_frames * 1e3, 3), "bytes_written": written,
-            "path": "add_frame + take_frame + writer thread -> per-level raw files, fsync"}
+            "ms_per_frame": round(el / n_frames * 1e3, 3), "frames": n_frames,
+            "geometry": [list(g) for g in geo], "dtype": np.dtype(dtype).name,
+            "bytes_written": written, "sink_fs": fs,
+            "writes": "raw level files (level 0 and every pyramid level), not a Zarr store",
+            "path": "add_frame + take_frame(every level) + a writer thread per level -> "
+                    "per-level raw files, fsync'd"}
 
 
 def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device, dist=None,

@@ -194,6 +194,16 @@ int aqz_ds_wait(aqz_ds* ds);
 int aqz_ds_poll(aqz_ds* ds, int* done);
 
 /*
+ * Wait only until the pending aqz_ds_add_frame_async[_take] job no longer
+ * reads its host frame (the upload is done, or the add failed): the caller
+ * may then reuse or free that frame, while the pyramid and the takes may
+ * still run.  Returns AQZ_OK (also when nothing is pending) and clears no
+ * status: a failed add is still reported by aqz_ds_wait.  No reference
+ * counterpart; aqz_node_wait_input is built on it.
+ */
+int aqz_ds_wait_input(aqz_ds* ds);
+
+/*
  * One level's part in aqz_ds_add_frame_async_take.
  *   mode AQZ_TAKE_NONE: nothing (the level is taken later, or not at all);
  *   AQZ_TAKE_INTO: right behind the add, take the level's frame if it has
@@ -636,6 +646,40 @@ int aqz_node_run_host_batch(aqz_node* node,
                             void* const* host_out_levels,
                             uint32_t* out_counts);
 
+/* aqz_node_run_device_batch flag: stage every block through the handle's
+ * own buffers even on the batch's GPU (tests the xGMI path on one GPU). */
+#define AQZ_NODE_STAGE_ALL 1u
+
+/*
+ * Device-resident batch over the node's GPUs (BASELINE config F: frame
+ * batches sharded across GPUs over xGMI).  `device_frames` and every
+ * `device_out_levels[L]` (index 0 ignored) live on HIP device `src_device`;
+ * results, layout and counts are those of aqz_ds_run_device_batch on one
+ * handle: the k-th frame emitted at level L at `device_out_levels[L] +
+ * k * level_bytes(L)`, so every level comes back in frame-id order, as
+ * Array::write_frame requires (array.cpp:179-189).  `n_frames` is a whole
+ * number of shard units and the node's stream stands on a unit boundary
+ * (else AQZ_INVALID_ARGUMENT before anything runs); adds in flight are
+ * flushed first.  Contiguous blocks of whole units go one per handle: a
+ * handle on `src_device` runs its block in place on `hip_stream`; a handle on
+ * another GPU pulls its block into its own staging by peer copy (xGMI DMA),
+ * runs it there and pushes each level back, in sub-batches of at most
+ * $AQZ_NODE_STAGE_MB MiB per staging slot (default 256) so that pull,
+ * pyramid and push overlap.  Asynchronous: the blocks start behind the work
+ * already on `hip_stream` (NULL = the null stream of `src_device`), and
+ * `hip_stream` waits for every block before its later work runs; the call
+ * returns without a host synchronisation.  `flags`: 0 or AQZ_NODE_STAGE_ALL.
+ * The caller's current device is unchanged on return.
+ */
+int aqz_node_run_device_batch(aqz_node* node,
+                              const void* device_frames,
+                              int src_device,
+                              uint32_t n_frames,
+                              void* const* device_out_levels,
+                              uint32_t* out_counts,
+                              void* hip_stream,
+                              uint32_t flags);
+
 /*
  * Streaming over the node: several frames in flight, one per handle.  Frame k
  * goes to handle (k / unit) % n_handles as an aqz_ds_add_frame_async_take that
@@ -664,8 +708,30 @@ int aqz_node_take_frame(aqz_node* node,
                         size_t* nbytes,
                         int* has_frame);
 
+/*
+ * Streaming takes of `level` chunk-tiled (tile_rows x tile_cols, the layout
+ * of aqz_ds_take_frame_tiled, zero overhang included) instead of row-major:
+ * aqz_node_take_frame then hands out the tiled frame.  Each handle tiles on
+ * its GPU right behind the pyramid (aqz_ds_set_level_tiling).  Before the
+ * first add only; (0, 0) restores row-major.
+ */
+int aqz_node_set_level_tiling(aqz_node* node,
+                              uint32_t level,
+                              uint32_t tile_rows,
+                              uint32_t tile_cols);
+
 /* Wait for every add in flight; their level frames become takeable. */
 int aqz_node_flush(aqz_node* node);
+
+/*
+ * Wait until no add in flight still reads its host frame (aqz_ds_wait_input
+ * on every handle): every frame handed to aqz_node_add_frame so far may then
+ * be reused, while their pyramids and level copies still run.  A failed add
+ * is reported by the take or flush that settles it.  The drop-in
+ * (integration/src/streaming/downsampler.hip.cpp, node mode) calls it where
+ * the single-handle adapter waits for the whole add.
+ */
+int aqz_node_wait_input(aqz_node* node);
 
 /* Last error message of the node (never NULL; "" when none). */
 const char* aqz_node_last_error(const aqz_node* node);

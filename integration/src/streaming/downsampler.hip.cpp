@@ -13,10 +13,26 @@
 //   wait()                       new                      -> aqz_ds_wait
 //   take_frame_tiled(level, t)   new -> aqz_ds_take_frame_tiled
 //   level_is_tiled(level)        new
+//   flush()                      new                      -> (node mode) aqz_node_flush
 //
 // take_frame on a level the add's background job already took tiled untiles
-// that copy on the host; add_frame_async settles a previous pending one
-// before it reuses the take buffers.
+// that copy on the host; add_frame and add_frame_async settle a previous
+// pending add first, so the levels it took are held before anything else
+// happens.
+//
+// Node mode ($AQZ_GPU_DEVICES with two or more HIP ordinals, e.g. "0,1,2,3"):
+// one aqz_node deals the stream's frames over those GPUs, so
+// several frames' pyramids and level copies run at once, each GPU over its
+// own PCIe link.  add_frame_async hands the frame to the next GPU and wait()
+// returns once it is uploaded (aqz_node_wait_input), not when its levels are
+// done; take_frame / take_frame_tiled hand out, in emission order, the next
+// level frame that is ready.  The patched MultiscaleArray takes every ready
+// frame per level after each add and calls flush() before it closes its
+// arrays, so each level receives exactly the frames, in the order, that the
+// reference's add_frame + take_frame loop produces (multiscale.array.cpp:
+// 291-325).  Z planes still waiting for their pair at close are dropped, as
+// the reference drops them.  A caller that skips takes gets no emplace drop
+// in this mode: the node takes every frame.
 //
 // The rest of the class stays in the reference's downsampler.cpp, compiled
 // unchanged: acquire-zarr-hip.patch only puts the CPU constructor, add_frame,
@@ -35,15 +51,54 @@
 
 #include "downsampler.hh"
 #include "macros.hh"
+#include "zarr.common.hh"
 
 #include "aqz_downsampler.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace {
+
+// $AQZ_GPU_DEVICES as HIP ordinals ("0,1,2"); fewer than two: no node.
+std::vector<int>
+node_devices()
+{
+    std::vector<int> devs;
+    const char* env = std::getenv("AQZ_GPU_DEVICES");
+    if (!env) {
+        return devs;
+    }
+    const std::string s(env);
+    size_t pos = 0;
+    while (pos <= s.size()) {
+        const size_t end = std::min(s.find(',', pos), s.size());
+        const std::string item = s.substr(pos, end - pos);
+        if (!item.empty()) {
+            size_t used = 0;
+            int d = -1;
+            try {
+                d = std::stoi(item, &used);
+            } catch (const std::exception&) {
+                used = 0;
+            }
+            EXPECT(used == item.size() && d >= 0,
+                   "GPU downsampler: bad entry in AQZ_GPU_DEVICES: '",
+                   item,
+                   "'");
+            devs.push_back(d);
+        }
+        pos = end + 1;
+    }
+    if (devs.size() < 2) {
+        devs.clear();
+    }
+    return devs;
+}
 
 // The reference validates the dtype before the method, with these messages
 // (downsampler.cpp:295-302).
@@ -79,51 +134,92 @@ zarr::Downsampler::Downsampler(std::shared_ptr<ArrayConfig> config,
         levels[level].planes = dims->at(dims->ndims() - 3).array_size_px;
     }
 
-    aqz_ds* handle = nullptr;
-    const int rc = aqz_ds_create(levels.data(),
-                                 static_cast<uint32_t>(n),
-                                 static_cast<int>(config->dtype),
-                                 static_cast<int>(method),
-                                 -1, // $AQZ_GPU_DEVICE, else the current device
-                                 &handle);
-    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_last_error());
-    gpu_ = handle;
+    tiles_.assign(n, { 0u, 0u });
+    takes_.assign(n, aqz_level_take{});
+    taken_.assign(n, {});
+    holding_.assign(n, 0);
+
+    if (const std::vector<int> devs = node_devices(); !devs.empty()) {
+        aqz_node* node = nullptr;
+        const int rc = aqz_node_create(levels.data(),
+                                       static_cast<uint32_t>(n),
+                                       static_cast<int>(config->dtype),
+                                       static_cast<int>(method),
+                                       devs.data(),
+                                       static_cast<uint32_t>(devs.size()),
+                                       &node);
+        EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_last_error());
+        node_ = node;
+    } else {
+        aqz_ds* handle = nullptr;
+        const int rc = aqz_ds_create(levels.data(),
+                                     static_cast<uint32_t>(n),
+                                     static_cast<int>(config->dtype),
+                                     static_cast<int>(method),
+                                     -1, // $AQZ_GPU_DEVICE, else the current device
+                                     &handle);
+        EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_last_error());
+        gpu_ = handle;
+    }
 
     // Levels >= 1 are tiled on the GPU right behind the pyramid, in their
     // own chunk shape (downsample_dimension keeps chunk sizes), so that
     // MultiscaleArray can hand each tile to its chunk in one copy
     // (array.tiled.cpp).  A transposed storage order keeps the row-major
     // path: Array chunks the transpose of what it is given.
-    tiles_.assign(n, { 0u, 0u });
-    takes_.assign(n, aqz_level_take{});
-    taken_.assign(n, {});
-    holding_.assign(n, 0);
     if (config->dimensions->needs_xy_transposition()) {
         return;
     }
-    for (size_t level = 1; level < n; ++level) {
-        const auto& dims = writer_configurations_.at(int(level))->dimensions;
-        const uint32_t tile_rows = dims->height_dim().chunk_size_px;
-        const uint32_t tile_cols = dims->width_dim().chunk_size_px;
-        if (tile_rows == 0 || tile_cols == 0) {
-            continue;
+    try {
+        for (size_t level = 1; level < n; ++level) {
+            const auto& dims = writer_configurations_.at(int(level))->dimensions;
+            const uint32_t tile_rows = dims->height_dim().chunk_size_px;
+            const uint32_t tile_cols = dims->width_dim().chunk_size_px;
+            if (tile_rows == 0 || tile_cols == 0) {
+                continue;
+            }
+            if (node_) {
+                EXPECT(aqz_node_set_level_tiling(
+                         node_, uint32_t(level), tile_rows, tile_cols) == AQZ_OK,
+                       "GPU downsampler: ",
+                       aqz_node_last_error(node_));
+            } else {
+                EXPECT(aqz_ds_set_level_tiling(
+                         gpu_, uint32_t(level), tile_rows, tile_cols) == AQZ_OK,
+                       "GPU downsampler: ",
+                       aqz_ds_last_error(gpu_));
+            }
+            tiles_[level] = { tile_rows, tile_cols };
         }
-        EXPECT(aqz_ds_set_level_tiling(
-                 gpu_, uint32_t(level), tile_rows, tile_cols) == AQZ_OK,
-               "GPU downsampler: ",
-               aqz_ds_last_error(gpu_));
-        tiles_[level] = { tile_rows, tile_cols };
+    } catch (...) {
+        // no destructor runs for a throwing constructor
+        aqz_node_destroy(node_);
+        aqz_ds_destroy(gpu_);
+        node_ = nullptr;
+        gpu_ = nullptr;
+        throw;
     }
 }
 
 zarr::Downsampler::~Downsampler()
 {
-    aqz_ds_destroy(gpu_); // settles a pending add_frame_async first
+    aqz_node_destroy(node_); // each handle settles its add in flight first
+    aqz_ds_destroy(gpu_);    // settles a pending add_frame_async first
 }
 
 void
 zarr::Downsampler::add_frame(std::vector<uint8_t>& frame)
 {
+    if (node_) {
+        add_frame_async(frame);
+        wait(); // the frame is uploaded; its levels come when ready
+        return;
+    }
+    // a pending add_frame_async first: its takes mark the levels they took
+    // as held, which decides where this frame's levels may go
+    if (pending_) {
+        wait();
+    }
     for (const uint8_t h : holding_) {
         if (h) {
             // frames taken ahead are still unconsumed: their levels must drop
@@ -140,6 +236,14 @@ zarr::Downsampler::add_frame(std::vector<uint8_t>& frame)
 void
 zarr::Downsampler::add_frame_async(std::vector<uint8_t>& frame)
 {
+    if (node_) {
+        // the previous frame may still be uploading to its GPU; this one
+        // goes to the next GPU in the deal
+        const int rc = aqz_node_add_frame(node_, frame.data(), frame.size());
+        EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+        pending_ = true;
+        return;
+    }
     // A previous add_frame_async may still be running its takes into takes_
     // and taken_: settle it (which also marks the levels it took as held)
     // before either is touched.
@@ -184,6 +288,13 @@ zarr::Downsampler::add_frame_async(std::vector<uint8_t>& frame)
 void
 zarr::Downsampler::wait()
 {
+    if (node_) {
+        // every frame handed over so far is uploaded: the caller may reuse it
+        pending_ = false;
+        const int rc = aqz_node_wait_input(node_);
+        EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+        return;
+    }
     const int rc = aqz_ds_wait(gpu_);
     const bool had_takes = pending_;
     pending_ = false;
@@ -213,18 +324,20 @@ zarr::Downsampler::hand_over_(int level, std::vector<uint8_t>& out)
 }
 
 void
-zarr::Downsampler::untile_held_(int level, std::vector<uint8_t>& out)
+zarr::Downsampler::untile_(int level,
+                           const std::vector<uint8_t>& tiled,
+                           std::vector<uint8_t>& out) const
 {
-    // taken_[level] holds the frame chunk-tiled (tile t = ty * n_tiles_x + tx,
+    // `tiled` holds a level frame chunk-tiled (tile t = ty * n_tiles_x + tx,
     // tile_rows x tile_cols, row-major, zero overhang); take_frame hands it
     // out row-major, as the reference's cached frame would be.
     const auto [tile_rows, tile_cols] = tiles_[level];
     const auto& dims = writer_configurations_.at(level)->dimensions;
     const size_t w = dims->width_dim().array_size_px;
     const size_t h = dims->height_dim().array_size_px;
-    const size_t bpp = aqz_ds_level_bytes(gpu_, uint32_t(level)) / (w * h);
+    const size_t bpp = zarr::bytes_of_type(writer_configurations_.at(level)->dtype);
     const size_t ntx = (w + tile_cols - 1) / tile_cols;
-    const uint8_t* tiles = taken_[level].data();
+    const uint8_t* tiles = tiled.data();
     out.resize(w * h * bpp);
     for (size_t y = 0; y < h; ++y) {
         const size_t ty = y / tile_rows, r = y % tile_rows;
@@ -237,7 +350,48 @@ zarr::Downsampler::untile_held_(int level, std::vector<uint8_t>& out)
                         n * bpp);
         }
     }
+}
+
+void
+zarr::Downsampler::untile_held_(int level, std::vector<uint8_t>& out)
+{
+    untile_(level, taken_[level], out);
     holding_[level] = 0;
+}
+
+bool
+zarr::Downsampler::node_take_(int level, std::vector<uint8_t>& out)
+{
+    // the next ready frame of the level, in emission order (tiled if the
+    // level is): size query, then the copy
+    size_t nbytes = 0;
+    int has_frame = 0;
+    int rc = aqz_node_take_frame(
+      node_, static_cast<uint32_t>(level), nullptr, 0, &nbytes, &has_frame);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+    if (!has_frame) {
+        return false;
+    }
+    out.resize(nbytes);
+    rc = aqz_node_take_frame(node_,
+                             static_cast<uint32_t>(level),
+                             out.data(),
+                             out.size(),
+                             &nbytes,
+                             &has_frame);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+    return has_frame != 0;
+}
+
+void
+zarr::Downsampler::flush()
+{
+    if (node_) {
+        const int rc = aqz_node_flush(node_);
+        EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+        return;
+    }
+    wait();
 }
 
 bool
@@ -247,6 +401,17 @@ zarr::Downsampler::take_frame(int level, std::vector<uint8_t>& frame_data)
     // including out-of-range ones (downsampler.cpp:403-414).
     if (level < 1 || static_cast<size_t>(level) >= n_levels_()) {
         return false;
+    }
+    if (node_) {
+        if (!level_is_tiled(level)) {
+            return node_take_(level, frame_data);
+        }
+        std::vector<uint8_t> tiled;
+        if (!node_take_(level, tiled)) {
+            return false;
+        }
+        untile_(level, tiled, frame_data);
+        return true;
     }
     if (pending_) {
         wait();
@@ -293,6 +458,9 @@ zarr::Downsampler::take_frame_tiled(int level, std::vector<uint8_t>& tiles)
 {
     if (!level_is_tiled(level)) {
         return false;
+    }
+    if (node_) {
+        return node_take_(level, tiles);
     }
     if (pending_) {
         wait();

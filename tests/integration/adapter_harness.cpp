@@ -22,6 +22,13 @@
 //               or not (a tiled level's background take is untiled)
 //     double    two add_frame_async calls back to back per pair of frames
 //               (the second settles the first), then the takes
+//     asyncsync as double, the second add synchronous (add_frame settles the
+//               pending add first: ADVICE r4)
+//     node      the patched MultiscaleArray with $AQZ_GPU_DEVICES naming
+//               several GPUs: add_frame_async, wait, then every READY frame
+//               per level (write_level_frames_); flush() and a last drain
+//               at the end (close_).  Only taken frames are written, `frame`
+//               = the add after which each came out; pattern must be "all"
 //   pattern: all | every3 (takes only after frames 2, 5, 8, ...)
 //   out.bin: per take, int64 {frame, level, has_frame, tiled, nbytes} then
 //            the bytes.
@@ -99,6 +106,24 @@ main(int argc, char** argv)
             }
         };
 
+        // node mode: every ready frame per level, in order, as the patched
+        // write_level_frames_ takes them
+        auto drain = [&](int k) {
+            for (int L = 1; L < n_levels; ++L) {
+                const bool tiled = ds.level_is_tiled(L);
+                for (;;) {
+                    std::vector<uint8_t> b;
+                    if (!(tiled ? ds.take_frame_tiled(L, b) : ds.take_frame(L, b)))
+                        break;
+                    emit(out, k, L, true, tiled, b);
+                }
+            }
+        };
+        if (mode == "node" && pattern != "all") {
+            std::fprintf(stderr, "node mode takes every frame: pattern must be all\n");
+            return 2;
+        }
+
         for (int k = 0; k < n_frames; ++k) {
             frame.assign(all.begin() + k * frame_bytes, all.begin() + (k + 1) * frame_bytes);
             if (mode == "sync") {
@@ -108,6 +133,21 @@ main(int argc, char** argv)
                 ds.add_frame_async(frame);
                 ds.wait();
                 takes(k, mode == "overlap");
+            } else if (mode == "node") {
+                ds.add_frame_async(frame);
+                ds.wait();
+                drain(k);
+            } else if (mode == "asyncsync") {
+                // frame k async; if the pattern takes nothing after it, frame
+                // k+1 goes in synchronously right behind it, no wait between
+                ds.add_frame_async(frame);
+                if (k + 1 < n_frames && !(pattern == "all" || k % 3 == 2)) {
+                    ++k;
+                    frame2.assign(all.begin() + k * frame_bytes,
+                                  all.begin() + (k + 1) * frame_bytes);
+                    ds.add_frame(frame2);
+                }
+                takes(k, true);
             } else if (mode == "double") {
                 // frame k async; if the pattern takes nothing after it, the
                 // next frame's add_frame_async must settle it first
@@ -125,6 +165,10 @@ main(int argc, char** argv)
             }
         }
         ds.wait();
+        if (mode == "node") {
+            ds.flush(); // MultiscaleArray::close_
+            drain(n_frames);
+        }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "adapter threw: %s\n", e.what());
         return 3;

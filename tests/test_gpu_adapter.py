@@ -16,7 +16,15 @@ the patched write_frame):
 * rowmajor — add_frame_async, wait, take_frame on levels the background job
              took tiled (ADVICE r3: untiled on the host);
 * double   — two add_frame_async calls back to back (the second
-             settles the first before reusing its take buffers).
+             settles the first before reusing its take buffers);
+* asyncsync — add_frame_async then add_frame with no wait between (ADVICE
+             r4: add_frame settles the pending add first, so the levels it
+             took are held and the second frame's are dropped there);
+* node     — $AQZ_GPU_DEVICES=0,0 (two handles on one GPU standing in for a
+             node's GPUs): the adapter over aqz_node, driven as the patched
+             MultiscaleArray drives it — every ready frame per level after each
+             add, flush() and a last drain at close.  Per level, the frames must
+             be exactly the reference's, in the reference's order.
 
 Every take is compared with the frames the REFERENCE ITSELF made for the same
 inputs (tests/golden/reference_vectors.*), row-major or tiled by the oracle's
@@ -50,10 +58,17 @@ def _cases():
         out.append((g, "float32", 1, "sync"))
         out.append((g, "int64", 1, "double"))
         out.append((g, "uint8", 0, "rowmajor"))
+        if MAN["geometries"][g]["take"] != "all":
+            out.append((g, "uint16", 1, "asyncsync"))
+            out.append((g, "float32", 2, "asyncsync"))
     for g in rv.NAN_GEOMETRIES:
         out.append(("nan:" + g, "float32", 1, "overlap"))
         out.append(("nan:" + g, "float64", 1, "sync"))
     return out
+
+
+NODE_CASES = [(g, d, m) for g in rv.GEOMETRIES if MAN["geometries"][g]["take"] == "all"
+              for d, m in (("uint16", 1), ("float32", 1), ("uint8", 3), ("int64", 2))]
 
 
 def _vec(geom):
@@ -66,7 +81,7 @@ def _vec(geom):
 CASES = _cases()
 
 
-def _run(tmp_path, geom, dtype, method, mode):
+def _run(tmp_path, geom, dtype, method, mode, env=None):
     vec, geom = _vec(geom)
     g = MAN["geometries"][geom]
     frames = vec[f"in/{geom}/{dtype}"]
@@ -76,7 +91,7 @@ def _run(tmp_path, geom, dtype, method, mode):
             f"{frames.shape[0]} {mode} {g['take']}\n" +
             "".join(f"{d[0]} {d[1]} {d[2]} {d[3]}\n" for d in g["dims"]))
     r = subprocess.run([HARNESS, str(fin), str(fout)], input=spec, capture_output=True,
-                       text=True, timeout=60)
+                       text=True, timeout=60, env=None if env is None else {**os.environ, **env})
     assert r.returncode == 0, r.stdout + r.stderr
     raw = fout.read_bytes()
     events, pos = [], 0
@@ -124,6 +139,45 @@ def test_adapter_matches_reference(tmp_path, oracle, geom, dtype, method, mode):
         assert bad is None, f"{ctx}: {bad.size} elements differ, first at {bad[0]}"
     if mode in ("overlap", "double"):
         assert n_tiled > 0
+
+
+@pytest.mark.skipif(not os.path.exists(HARNESS), reason="adapter harness not built")
+@pytest.mark.parametrize("geom,dtype,method", NODE_CASES,
+                         ids=[f"{g}-{d}-{rv.METHOD_NAMES[m]}" for g, d, m in NODE_CASES])
+def test_adapter_node_mode_matches_reference(tmp_path, oracle, geom, dtype, method):
+    got = _run(tmp_path, geom, dtype, method, "node", env={"AQZ_GPU_DEVICES": "0,0"})
+    g = MAN["geometries"][geom]
+    dt = np.dtype(dtype)
+    name = f"{geom}/{dtype}/{rv.METHOD_NAMES[method]}"
+    ev, out = VEC[f"ev/{name}"], VEC[f"out/{name}"]
+    # the reference's frames per level, in emission order
+    want = {L: [] for L in range(1, len(g["levels"]))}
+    off = 0
+    for k, L, has, nb in ev:
+        if has:
+            want[int(L)].append(out[off:off + int(nb)])
+            off += int(nb)
+    by_level = {L: [] for L in want}
+    for k, L, has, tiled, b in got:
+        assert has
+        by_level[L].append((k, tiled, b))
+    for L, frames_L in want.items():
+        assert len(by_level[L]) == len(frames_L), f"{name} node: level {L}"
+        lv = g["levels"][L]
+        w, h = lv[-1][1], lv[-2][1]
+        for i, ((_, tiled, b), wb) in enumerate(zip(by_level[L], frames_L)):
+            if tiled:
+                tiles, _ = oracle.tile_frame(wb.view(dt).reshape(h, w), lv[-2][2], lv[-1][2])
+                wb = tiles.view(np.uint8).reshape(-1)
+            bad = rv.same(b, wb, dt, nan_bits=True)
+            assert bad is None, f"{name} node: level {L} frame {i}: {bad.size} elements differ"
+
+
+@pytest.mark.skipif(not os.path.exists(HARNESS), reason="adapter harness not built")
+def test_adapter_node_mode_rejects_bad_device_list(tmp_path):
+    with pytest.raises(AssertionError) as e:
+        _run(tmp_path, "xy_even_64x48", "uint16", 1, "node", env={"AQZ_GPU_DEVICES": "0,x"})
+    assert "AQZ_GPU_DEVICES" in str(e.value)
 
 
 @pytest.mark.skipif(not os.path.exists(HARNESS), reason="adapter harness not built")

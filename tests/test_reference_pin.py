@@ -12,7 +12,12 @@ the reference) are checked wherever the suite runs:
   writer_configurations() level by level, scales included;
 * the product's method strings and metadata JSON equal the reference's
   downsampling_method() and get_metadata().dump(), byte for byte, and its
-  create errors carry the reference's messages;
+  create errors carry the reference's messages.  Caveat: the
+  reference build in oracle/_ref links the image's nlohmann/json 3.1.1,
+  while the reference's vcpkg.json asks for >= 3.11.3 — so the dump() bytes
+  are pinned against a 3.1.1 build only, and unpinned against a supported
+  nlohmann/json (the metadata holds strings and small integers only, whose
+  serialisation the two versions share, but no 3.11 build ran here);
 * the oracle-made digests of the BASELINE configs equal the reference-made
   ones.
 
