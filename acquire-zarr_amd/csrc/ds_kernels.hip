@@ -11,13 +11,16 @@
 // divide by 4 (exact as a multiply by 0.25), min/max are compare-select
 // chains seeded with the first operand so NaN order matches.
 //
-// Design: this is an HBM-bound stencil, not a contraction — no MFMA, no LDS
-// staging.  Each wave owns a tile of 64 lanes x 16 bytes wide and 2^NL rows
-// tall, issues all 2^NL row loads (16 B per lane, 1 KiB per wave
-// instruction) before any arithmetic, and reduces the pyramid in registers:
-// in-lane while a lane still holds >= 2 columns of a level, then across lanes
-// with __shfl_down at doubling strides.  Every level of the run is written
-// from the same pass, so the base frame is read exactly once.
+// Design: this is an HBM-bound stencil, not a contraction — no MFMA.  Each
+// wave owns a tile of 64 lanes x 16 bytes wide and 2^NL rows tall, issues
+// all 2^NL row loads (16 B per lane, 1 KiB per wave instruction) before any
+// arithmetic, and reduces the pyramid in registers: in-lane while a lane
+// still holds >= 2 columns of a level, then across lanes with __shfl_down at
+// doubling strides.  Every level of the run is written from the same pass,
+// so the base frame is read exactly once.  LDS only assembles stores: the
+// band kernels (cascade_band_kernel) stage each level's rows of a whole row
+// band in LDS so that they leave as full 64-byte bursts, and
+// transpose_kernel turns its tiles through LDS.
 #include "ds_kernels.hh"
 
 // Build sharding (acquire-zarr_amd/Makefile): the library compiles this file
@@ -1522,21 +1525,21 @@ volume_level(const VolumeParams& p,
     }
 }
 
-// C = columns per lane (V = C*sizeof(T)/16 loads per row); ZFAST puts the
-// plane group innermost in the unit order.
-template<typename T, int M, int NL, int C, bool EDGE>
+// C = columns per lane (V = C*sizeof(T)/16 loads per row).  NTL: loads
+// nontemporal.  Decimate reads planes 0 and 2 and rows 0 and 2 of the unit
+// only (the other loads have no use and are dropped by the compiler).
+template<typename T, int M, int NL, int C, bool EDGE, bool NTL>
 __device__ __forceinline__ void
-volume_unit(const VolumeParams& p,
+volume_load(const VolumeParams& p,
             uint32_t g,
             uint32_t row0,
             uint32_t col0,
-            int lane)
+            T (&v)[1 << NL][1 << NL][C])
 {
     constexpr int R = 1 << NL;
     constexpr int Z = 1 << NL;
     constexpr int V = C * int(sizeof(T)) / 16;
     const bool last_group = g + 1 == p.total_units / (p.units_x * p.units_y);
-    T v[Z][R][C];
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
         const T* src = reinterpret_cast<const T*>(p.src) +
@@ -1546,28 +1549,38 @@ volume_unit(const VolumeParams& p,
 #pragma unroll
             for (int k = 0; k < V; ++k) {
                 constexpr int E = 16 / int(sizeof(T));
-                load_chunk<T, E, true, EDGE>(&v[z][r][k * E], src + uint64_t(row0 + r) * p.W,
-                                             col0 + uint32_t(k) * E, p.W, row0 + r < p.H,
-                                             !(last_group && z == Z - 1) ||
-                                               row0 + r + 1 < p.H);
+                load_chunk<T, E, NTL, EDGE>(&v[z][r][k * E], src + uint64_t(row0 + r) * p.W,
+                                            col0 + uint32_t(k) * E, p.W, row0 + r < p.H,
+                                            !(last_group && z == Z - 1) ||
+                                              row0 + r + 1 < p.H);
             }
         }
     }
-    volume_level<T, M, C, 1, NL, Z, R, C, EDGE, true>(p, v, g, row0, col0, lane);
 }
 
-// ZFAST puts the plane group innermost in the unit order.
-template<typename T, int M, int NL, int C = 16 / int(sizeof(T)), bool ZFAST = false>
-__global__ __launch_bounds__(256) void
-volume_kernel(VolumeParams p)
+template<typename T, int M, int NL, int C, bool EDGE, bool NTL>
+__device__ __forceinline__ void
+volume_unit(const VolumeParams& p,
+            uint32_t g,
+            uint32_t row0,
+            uint32_t col0,
+            int lane)
 {
     constexpr int R = 1 << NL;
-    const int lane = threadIdx.x & 63;
-    const uint32_t u =
-      blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (u >= p.total_units)
-        return;
-    uint32_t ux, uy, g;
+    T v[R][R][C];
+    volume_load<T, M, NL, C, EDGE, NTL>(p, g, row0, col0, v);
+    volume_level<T, M, C, 1, NL, R, R, C, EDGE, true>(p, v, g, row0, col0, lane);
+}
+
+// Unit u's plane group, first row and this lane's first column; true when
+// the unit lies wholly inside the frame.  ZFAST puts the plane group
+// innermost in the unit order.
+template<int NL, int C, bool ZFAST>
+__device__ __forceinline__ bool
+volume_coords(const VolumeParams& p, uint32_t u, int lane, uint32_t& g, uint32_t& row0,
+              uint32_t& col0)
+{
+    uint32_t ux, uy;
     if constexpr (ZFAST) {
         const uint32_t groups = p.total_units / (p.units_x * p.units_y);
         g = u % groups;
@@ -1580,13 +1593,64 @@ volume_kernel(VolumeParams p)
         uy = t % p.units_y;
         g = t / p.units_y;
     }
-    const uint32_t row0 = uy * R;
+    row0 = uy * (1u << NL);
     const uint32_t tile_col0 = ux * (64u * C);
-    const uint32_t col0 = tile_col0 + uint32_t(lane) * C;
-    if ((tile_col0 + 64u * C <= p.W) && (row0 + R <= p.H)) {
-        volume_unit<T, M, NL, C, false>(p, g, row0, col0, lane);
+    col0 = tile_col0 + uint32_t(lane) * C;
+    return (tile_col0 + 64u * C <= p.W) && (row0 + (1u << NL) <= p.H);
+}
+
+// NTL: nontemporal loads.  UPW units per wave (consecutive, columns first):
+// with UPW > 1 and every unit inside the frame, all of them are loaded
+// before the first is reduced, so a wave has UPW units' loads in flight —
+// Decimate's units read only 4 KiB.  Round 5: Decimate's
+// volume launch ran at 0.64 of spec with nontemporal loads and 0.82-0.86
+// with plain ones (tools/volume_probe.hip).
+template<typename T, int M, int NL, bool NTL, int UPW, int C = 16 / int(sizeof(T)),
+         bool ZFAST = false>
+__global__ __launch_bounds__(256) void
+volume_kernel(VolumeParams p)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t w =
+      blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr (UPW == 1) {
+        if (w >= p.total_units)
+            return;
+        uint32_t g, row0, col0;
+        if (volume_coords<NL, C, ZFAST>(p, w, lane, g, row0, col0))
+            volume_unit<T, M, NL, C, false, NTL>(p, g, row0, col0, lane);
+        else
+            volume_unit<T, M, NL, C, true, NTL>(p, g, row0, col0, lane);
     } else {
-        volume_unit<T, M, NL, C, true>(p, g, row0, col0, lane);
+        constexpr int R = 1 << NL;
+        const uint32_t u0 = w * UPW;
+        if (u0 >= p.total_units)
+            return;
+        uint32_t g[UPW], row0[UPW], col0[UPW];
+        bool inside = u0 + UPW <= p.total_units;
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) {
+            const uint32_t u = min(u0 + uint32_t(i), p.total_units - 1);
+            inside = volume_coords<NL, C, ZFAST>(p, u, lane, g[i], row0[i], col0[i]) && inside;
+        }
+        if (inside) {
+            T v[UPW][R][R][C];
+#pragma unroll
+            for (int i = 0; i < UPW; ++i)
+                volume_load<T, M, NL, C, false, NTL>(p, g[i], row0[i], col0[i], v[i]);
+#pragma unroll
+            for (int i = 0; i < UPW; ++i)
+                volume_level<T, M, C, 1, NL, R, R, C, false, true>(p, v[i], g[i], row0[i],
+                                                                   col0[i], lane);
+        } else {
+            for (int i = 0; i < UPW && u0 + uint32_t(i) < p.total_units; ++i) {
+                uint32_t gg, r0, c0;
+                if (volume_coords<NL, C, ZFAST>(p, u0 + uint32_t(i), lane, gg, r0, c0))
+                    volume_unit<T, M, NL, C, false, NTL>(p, gg, r0, c0, lane);
+                else
+                    volume_unit<T, M, NL, C, true, NTL>(p, gg, r0, c0, lane);
+            }
+        }
     }
 }
 
@@ -2713,13 +2777,42 @@ AQZ_SHARDED(launch_volume)(int dtype,
             p.w[i] = outs[i].w;
             p.h[i] = outs[i].h;
         }
-        const uint32_t grid = grid_for(total, 4, 0);
+        // Load policy and units per wave: Decimate's
+        // every-other-row, every-other-plane reads run 25% faster with plain
+        // loads than nontemporal ones, and its 4-KiB units two to a wave;
+        // $AQZ_VOLUME_NT=0/1 and $AQZ_VOLUME_UPW=1/2 (Decimate) override.
+        static const int nt_env = int_env("AQZ_VOLUME_NT", -1);
+        static const int upw_env = int_env("AQZ_VOLUME_UPW", 0);
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            if (n_out == 1)
-                hipLaunchKernelGGL((volume_kernel<T, M, 1>), dim3(grid), dim3(256), 0, stream, p);
+            const bool ntl = nt_env >= 0 ? nt_env != 0 : M != kDecimate;
+            const int upw = M == kDecimate ? (upw_env > 0 ? std::min(upw_env, 2) : 2) : 1;
+            const uint32_t grid = grid_for((total + upw - 1) / upw, 4, 0);
+#define AQZ_VOL(NL, NTL, UPW)                                                          \
+    hipLaunchKernelGGL((volume_kernel<T, M, NL, NTL, UPW>), dim3(grid), dim3(256), 0, \
+                       stream, p)
+            if constexpr (M == kDecimate) {
+                if (upw == 2) {
+                    if (n_out == 1 && ntl)
+                        AQZ_VOL(1, true, 2);
+                    else if (n_out == 1)
+                        AQZ_VOL(1, false, 2);
+                    else if (ntl)
+                        AQZ_VOL(2, true, 2);
+                    else
+                        AQZ_VOL(2, false, 2);
+                    return hipGetLastError();
+                }
+            }
+            if (n_out == 1 && ntl)
+                AQZ_VOL(1, true, 1);
+            else if (n_out == 1)
+                AQZ_VOL(1, false, 1);
+            else if (ntl)
+                AQZ_VOL(2, true, 1);
             else
-                hipLaunchKernelGGL((volume_kernel<T, M, 2>), dim3(grid), dim3(256), 0, stream, p);
+                AQZ_VOL(2, false, 1);
+#undef AQZ_VOL
             return hipGetLastError();
         });
     });
