@@ -2236,6 +2236,16 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         p.remap = xcd_remap_env() == 1;
         p.wb = store_wb_env() >= 0 ? uint32_t(store_wb_env()) : 0u;
         p.nt = load_nt(W, sizeof(T));
+        // Decimate waves that loop over small units (half of each unit's rows
+        // read) load plain, not nontemporal: 512^2 u8 Decimate (4 units per
+        // wave) 37.0 -> 33.7 us, 0.89 -> 0.99 of the same-mix ceiling, as the
+        // volume Decimate (launch_volume).  Everything else measured keeps
+        // the nontemporal hint on aligned rows: 4096^2 u16 / f32 and 2048^2
+        // u16 Decimate (one 4-KiB unit per wave) 290 / 605 / 67.6 us with it
+        // against 306 / 653 / 80.3 without, Mean 5-20% slower without it
+        // (profiles/r05/decnt/ab.log).
+        if (load_nt_env() < 0 && method == kDecimate && p.upw > 1)
+            p.nt = 0;
         // Band staging when some level's rows are not whole 64-byte bursts
         // and a row band is at most 4 tiles, 6 for 2-byte types
         // ($AQZ_BAND_STAGING=0: never; $AQZ_BAND_MIS_MAX: the widest such

@@ -891,48 +891,56 @@ def measure_blosc_frames(aqz, torch, threads=16, n_chunks=256, reps=5):
 
 def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
     """Measured HBM ceiling for the kernel's own byte mix (tools/hbm_probe.hip):
-    a contiguous non-temporal stream reading the same input buffer and writing
-    in the nearest of the ratios 12:4, 13:3, 14:2, 10:6, 9:7 (4 KiB blocks per
-    workgroup), plus a read-only pass, timed with HIP events on the launch
-    stream.  A measurement aid, not product code: skipped (None) if the probe
-    library was not built."""
+    a contiguous stream reading the same input buffer and writing (non-
+    temporal stores) in the nearest of the ratios 12:4, 13:3, 14:2, 10:6, 9:7
+    (4 KiB blocks per workgroup), plus a read-only pass, timed with HIP events
+    on the launch stream.  Round 5: each pass runs with nontemporal and with
+    plain loads and the faster counts (plain loads beat nontemporal ones on
+    the volume Decimate launch), so the ceiling is the best
+    of both policies.  A measurement aid, not product code: skipped (None) if
+    the probe library was not built."""
     import ctypes
     path = os.path.join(ROOT, "tools", "libaqz_hbm_probe.so")
     if not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
-    lib.aqz_hbm_probe.restype = ctypes.c_int
-    lib.aqz_hbm_probe.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    lib.aqz_hbm_probe_ld.restype = ctypes.c_int
+    lib.aqz_hbm_probe_ld.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     frac_r = read_bytes / max(1, read_bytes + write_bytes)
     rd, wr = min(((12, 4), (13, 3), (14, 2), (10, 6), (9, 7)), key=lambda m: abs(m[0] / 16 - frac_r))
     dst = torch.empty(read_bytes // rd * wr + 4096, dtype=torch.uint8, device="cuda")
     sink = torch.zeros(16, dtype=torch.uint8, device="cuda")
     out = {}
     for name, (r, w) in (("GBps", (rd, wr)), ("read_only_GBps", (16, 0))):
-        moved = ctypes.c_uint64(0)
+        best = {}
+        for nt in (1, 0):
+            moved = ctypes.c_uint64(0)
 
-        def go():
-            rc = lib.aqz_hbm_probe(d_in.data_ptr(), read_bytes, dst.data_ptr(),
-                                   sink.data_ptr(), r, w, stream.cuda_stream,
-                                   ctypes.byref(moved))
-            if rc != 0:
-                raise RuntimeError(f"aqz_hbm_probe failed: {rc}")
-        for _ in range(3):
-            go()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(reps)]
-        for a, b in ev:
-            a.record(stream)
-            go()
-            b.record(stream)
-        torch.cuda.synchronize()
-        us = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e3
-        out[name] = round(moved.value / (us * 1e-6) / 1e9, 1)
+            def go():
+                rc = lib.aqz_hbm_probe_ld(d_in.data_ptr(), read_bytes, dst.data_ptr(),
+                                          sink.data_ptr(), r, w, nt, stream.cuda_stream,
+                                          ctypes.byref(moved))
+                if rc != 0:
+                    raise RuntimeError(f"aqz_hbm_probe_ld failed: {rc}")
+            for _ in range(3):
+                go()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(reps)]
+            for a, b in ev:
+                a.record(stream)
+                go()
+                b.record(stream)
+            torch.cuda.synchronize()
+            us = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e3
+            best["nt" if nt else "plain"] = round(moved.value / (us * 1e-6) / 1e9, 1)
+        out[name] = max(best.values())
+        out[name + "_by_load"] = best
     out["read_write"] = f"{rd}:{wr}"
-    out["kernel"] = ("tools/hbm_probe.hip: contiguous nt loads/stores, one 4 KiB-block "
-                     "round per workgroup, same input buffer and stream")
+    out["kernel"] = ("tools/hbm_probe.hip: contiguous loads (best of nt and plain) and nt "
+                     "stores, one 4 KiB-block round per workgroup, same input buffer and "
+                     "stream")
     return out
 
 

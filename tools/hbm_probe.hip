@@ -1,7 +1,8 @@
 // tools/hbm_probe.hip — measured HBM ceilings for bench.py (not product).
 //
-// libaqz_hbm_probe.so exports one launcher: a contiguous, non-temporal
-// read + write stream with a fixed read:write byte ratio (RD:WR 4 KiB
+// libaqz_hbm_probe.so exports one launcher: a contiguous read + write stream
+// (non-temporal stores; loads non-temporal or plain, aqz_hbm_probe_ld) with a
+// fixed read:write byte ratio (RD:WR 4 KiB
 // blocks per 256-thread workgroup, one round per workgroup, every load of a
 // wave instruction one contiguous KiB).  tools/readbench.hip and
 // tools/variants.hip measured this shape as the fastest way to move bytes
@@ -17,15 +18,19 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template<int RD, int WR>
+template<int RD, int WR, bool NTL = true>
 __global__ __launch_bounds__(256) void
 mix_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint32_t* sink)
 {
     const uint64_t rb = uint64_t(blockIdx.x) * 256 * RD + threadIdx.x;
     u32x4 v[RD];
 #pragma unroll
-    for (int k = 0; k < RD; ++k)
-        v[k] = __builtin_nontemporal_load(src + rb + k * 256);
+    for (int k = 0; k < RD; ++k) {
+        if constexpr (NTL)
+            v[k] = __builtin_nontemporal_load(src + rb + k * 256);
+        else
+            v[k] = src[rb + k * 256];
+    }
     if constexpr (WR == 0) {
         uint32_t acc = 0;
 #pragma unroll
@@ -151,8 +156,8 @@ aqz_hbm_probe_rows(const void* src, uint32_t row_bytes, uint64_t pitch, uint32_t
 // 4 bytes.  Supported RD:WR = 16:0, 12:4, 13:3, 14:2, 10:6, 9:7.  Returns 0 or a
 // hipError_t; *moved_bytes = bytes read + written.
 int
-aqz_hbm_probe(const void* src, uint64_t src_bytes, void* dst, void* sink, int rd, int wr,
-              void* stream, uint64_t* moved_bytes)
+aqz_hbm_probe_ld(const void* src, uint64_t src_bytes, void* dst, void* sink, int rd, int wr,
+                 int nt_load, void* stream, uint64_t* moved_bytes)
 {
     if (!src || !sink || (wr && !dst) || rd <= 0)
         return int(hipErrorInvalidValue);
@@ -163,23 +168,34 @@ aqz_hbm_probe(const void* src, uint64_t src_bytes, void* dst, void* sink, int rd
     const auto* in = static_cast<const u32x4*>(src);
     auto* out = static_cast<u32x4*>(dst);
     auto* sk = static_cast<uint32_t*>(sink);
-    if (rd == 16 && wr == 0)
-        hipLaunchKernelGGL((mix_kernel<16, 0>), dim3(blocks), dim3(256), 0, s, in, out, sk);
-    else if (rd == 12 && wr == 4)
-        hipLaunchKernelGGL((mix_kernel<12, 4>), dim3(blocks), dim3(256), 0, s, in, out, sk);
-    else if (rd == 13 && wr == 3)
-        hipLaunchKernelGGL((mix_kernel<13, 3>), dim3(blocks), dim3(256), 0, s, in, out, sk);
-    else if (rd == 14 && wr == 2)
-        hipLaunchKernelGGL((mix_kernel<14, 2>), dim3(blocks), dim3(256), 0, s, in, out, sk);
-    else if (rd == 10 && wr == 6) // Decimate's mix: half the rows read
-        hipLaunchKernelGGL((mix_kernel<10, 6>), dim3(blocks), dim3(256), 0, s, in, out, sk);
-    else if (rd == 9 && wr == 7)
-        hipLaunchKernelGGL((mix_kernel<9, 7>), dim3(blocks), dim3(256), 0, s, in, out, sk);
-    else
-        return int(hipErrorInvalidValue);
-    if (moved_bytes)
-        *moved_bytes = blocks * uint64_t(rd + wr) * 4096;
-    return int(hipGetLastError());
+#define AQZ_MIX(R, W)                                                                     \
+    if (rd == R && wr == W) {                                                            \
+        if (nt_load)                                                                     \
+            hipLaunchKernelGGL((mix_kernel<R, W, true>), dim3(blocks), dim3(256), 0, s, in, \
+                               out, sk);                                                 \
+        else                                                                             \
+            hipLaunchKernelGGL((mix_kernel<R, W, false>), dim3(blocks), dim3(256), 0, s, \
+                               in, out, sk);                                             \
+        if (moved_bytes)                                                                 \
+            *moved_bytes = blocks * uint64_t(rd + wr) * 4096;                            \
+        return int(hipGetLastError());                                                   \
+    }
+    AQZ_MIX(16, 0)
+    AQZ_MIX(12, 4)
+    AQZ_MIX(13, 3)
+    AQZ_MIX(14, 2)
+    AQZ_MIX(10, 6) // Decimate's mix: half the rows read
+    AQZ_MIX(9, 7)
+#undef AQZ_MIX
+    return int(hipErrorInvalidValue);
+}
+
+// aqz_hbm_probe_ld with nontemporal loads (the round-1..4 ceiling).
+int
+aqz_hbm_probe(const void* src, uint64_t src_bytes, void* dst, void* sink, int rd, int wr,
+              void* stream, uint64_t* moved_bytes)
+{
+    return aqz_hbm_probe_ld(src, src_bytes, dst, sink, rd, wr, 1, stream, moved_bytes);
 }
 
 } // extern "C"
