@@ -84,8 +84,9 @@ enum
 // gives the positive quiet NaN), so the kernels keep
 // the plain arithmetic and rebuild the bits only where the result is a NaN:
 // one compare per output in the common case, the walk below when a wave has
-// a NaN lane.  The walk works on bits (integer ops) so nothing canonicalises
-// the payload; divide by 4 or 2 keeps a quiet NaN unchanged on x86.  The
+// a NaN lane.  The walk selects on bits (integer ops) so nothing
+// canonicalises the payload; divide by 4 or 2 keeps a quiet NaN unchanged on
+// x86.  The
 // oracle states the same rule (oracle/ds_oracle.c add_<T>).
 template<typename T>
 struct float_bits;
@@ -104,7 +105,7 @@ struct float_bits<double>
     static constexpr U default_nan() { return 0xFFF8000000000000ull; }
 };
 
-// x86 `x + y` with its NaN rule (x the first source).
+// x86 `x + y` with its NaN rule (x the first source), as selects on bits.
 template<typename T>
 __device__ __forceinline__ T
 x86_add(T x, T y)
@@ -112,32 +113,22 @@ x86_add(T x, T y)
     using FB = float_bits<T>;
     using U = typename FB::U;
     const T s = x + y;
-    U r;
-    if (x != x)
-        r = __builtin_bit_cast(U, x) | FB::quiet();
-    else if (y != y)
-        r = __builtin_bit_cast(U, y) | FB::quiet();
-    else if (s != s)
-        r = FB::default_nan();
-    else
-        return s;
-    return __builtin_bit_cast(T, r);
+    const U bx = __builtin_bit_cast(U, x) | FB::quiet();
+    const U by = __builtin_bit_cast(U, y) | FB::quiet();
+    const U bs = (s != s) ? FB::default_nan() : __builtin_bit_cast(U, s);
+    return __builtin_bit_cast(T, (x != x) ? bx : ((y != y) ? by : bs));
 }
 
-template<typename T>
-__device__ __forceinline__ T
-mean4_nan(T a, T b, T c, T d)
+// Whether any lane of the wave holds a NaN result.  The fix-up runs behind a
+// wave-uniform branch.  A lane-divergent one (only the NaN lanes inside) gave
+// wrong outputs in the 16-byte f32 tiles: other columns of the NaN lanes, at
+// frame edges, on 4 of 256 fuzz cases (round 5, tools/narrow_dbg.py; root
+// cause not isolated).  The uniform branch leaves the exec mask alone and
+// passes all of them.
+__device__ __forceinline__ bool
+wave_any(bool p)
 {
-    // a NaN result: the chain's first NaN is its value (x86 keeps it through
-    // the later adds and the divide)
-    return x86_add(x86_add(x86_add(a, b), c), d);
-}
-
-template<typename T>
-__device__ __forceinline__ T
-mean2_nan(T a, T b)
-{
-    return x86_add(a, b);
+    return __builtin_amdgcn_ballot_w64(p) != 0;
 }
 
 template<typename T>
@@ -146,8 +137,12 @@ mean4(T a, T b, T c, T d)
 {
     if constexpr (std::is_floating_point_v<T>) {
         const T r = (((a + b) + c) + d) / T(4);
-        if (__builtin_expect(r != r, 0))
-            return mean4_nan(a, b, c, d);
+        if (__builtin_expect(wave_any(r != r), 0)) {
+            // the chain's first NaN is the value (x86 keeps it through the
+            // later adds and the divide); other lanes keep theirs
+            const T n = x86_add(x86_add(x86_add(a, b), c), d);
+            return (r != r) ? n : r;
+        }
         return r;
     } else if constexpr (sizeof(T) < sizeof(int)) {
         return T((int(a) + int(b) + int(c) + int(d)) / 4);
@@ -164,8 +159,10 @@ mean2(T a, T b)
 {
     if constexpr (std::is_floating_point_v<T>) {
         const T r = (a + b) / T(2);
-        if (__builtin_expect(r != r, 0))
-            return mean2_nan(a, b);
+        if (__builtin_expect(wave_any(r != r), 0)) {
+            const T n = x86_add(a, b);
+            return (r != r) ? n : r;
+        }
         return r;
     } else if constexpr (sizeof(T) < sizeof(int)) {
         return T((int(a) + int(b)) / 2);
@@ -2149,6 +2146,22 @@ cascade_pick_cols(int dtype,
     const uint32_t cw = cascade_cols(b), cn = cw / 2;
     const bool wide = cascade_fits(b, src, src_frame_elems, W, H, outs, n_out, cw);
     const bool narrow = cascade_fits(b, src, src_frame_elems, W, H, outs, n_out, cn);
+    // 4-byte types on rows of whole 128-B lines take 16-byte tiles too (4
+    // columns per lane: 73 VGPRs, 6 waves per SIMD, against 138 VGPRs and 3
+    // waves for 32-byte tiles) now that such rows leave through LDS-staged
+    // bands: 4096^2 f32 Mean 985 -> 948 us, Max 992 -> 946, Decimate 604 ->
+    // 583, 8192x2048 947 -> 903, 3072^2 1105 -> 1018 (profiles/r05/narrow/;
+    // round 1, before band staging, had measured the opposite, 1083 -> 975
+    // us for the wide tiles).  Rows that split lines keep the wide tiles and
+    // their misaligned segments: 5472x3648 1091 against 1206 us narrow,
+    // 6000x4000 1049 against 1150, 2000^2 1085 against 1123.
+    // $AQZ_CASCADE_NARROW=0/1 (A/B) forces wide / narrow for 4- and 8-byte
+    // types.
+    static const int narrow_env = int_env("AQZ_CASCADE_NARROW", -1);
+    const bool prefer_narrow = narrow_env >= 0 ? (narrow_env != 0 && b >= 4)
+                                               : (b == 4 && (uint64_t(W) * b) % 128 == 0);
+    if (prefer_narrow && narrow)
+        return cn;
     if (wide && W >= 64 * cw)
         return cw;
     if (narrow)
@@ -2491,9 +2504,16 @@ cascade_tiled_cols(int dtype, uint32_t W)
     if (!b)
         return 0;
     const uint32_t cw = cascade_cols(b);
-    // $AQZ_TILED_NARROW (A/B): 1 half-width tiles wherever they fit, 0 wide
+    // $AQZ_TILED_NARROW (A/B): 1 half-width tiles wherever they fit, 0 wide;
+    // unset: half-width for 4-byte types on line-aligned rows, as
+    // cascade_pick_cols (the streaming path writes a run tiled in one launch
+    // only when both agree): chunk-tiled 4096^2 f32 964-979 against
+    // 995-1033 us wide; 5472x3648, 6000x4000 and 2000^2 keep wide tiles
+    // (1113 / 990 / 1031 against 1129 / 1074 / 1055 us narrow;
+    // profiles/r05/narrow/ab_shapes.log)
     static const int narrow = int_env("AQZ_TILED_NARROW", -1);
-    if (narrow == 1 && W >= 64 * (cw / 2))
+    if ((narrow == 1 || (narrow < 0 && b == 4 && (uint64_t(W) * b) % 128 == 0)) &&
+        W >= 64 * (cw / 2))
         return cw / 2;
     return W >= 64 * cw ? cw : cw / 2;
 }

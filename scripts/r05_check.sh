@@ -17,7 +17,7 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-m
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 600 python bench.py > $OUT/bench_headline.json 2> $OUT/bench_headline.err || { tail -20 $OUT/bench_headline.err; exit 1; }
 python -c "import json;d=json.load(open('$OUT/bench_headline.json'));r=d['roofline'];c=d['cpu_baseline'];e=d['e2e'];print(d['value'], d['ms_per_step'], r['frac'], r['avg_launch_us'], r['traffic'], r.get('same_mix_ceiling',{}).get('frac_of_ceiling'), c['kind'], c['value'], e['ms_per_frame'], e['c2_filesystem_sink']['ms_per_frame'])"
-for wm in 1024x1024x256_u16:decimate 512x512_u8:decimate; do
+for wm in ${WMS:-1024x1024x256_u16:decimate 512x512_u8:decimate}; do
   w=${wm%%:*}; m=${wm##*:}
   timeout -k 10 300 python bench.py --workload $w --method $m --steps 20 --warmup 5 --cpu-seconds 0 \
     --e2e-frames 0 > $OUT/m_${w}_$m.json 2> $OUT/m_${w}_$m.err || { tail -20 $OUT/m_${w}_$m.err; exit 1; }

@@ -43,6 +43,18 @@ def random_frames(rng, dtype, shape, specials=True):
         for val in (np.nan, np.inf, -np.inf, -0.0, 0.0, tiny / 8, -tiny / 3):
             idx = rng.integers(0, n, k)
             flat[idx] = dt.type(val)
+        # NaNs with random sign and payload, quiet and signaling, written as
+        # bits (a float conversion would quiet them): the reference binary's
+        # NaN choice must come out byte for byte
+        ut = np.dtype(f"u{dt.itemsize}")
+        mant = np.finfo(dt).nmant
+        bits = flat.view(ut)
+        idx = rng.integers(0, n, k)
+        exp = ut.type(((1 << (8 * dt.itemsize - 1 - mant)) - 1) << mant)
+        sign = rng.integers(0, 2, k).astype(ut) << ut.type(8 * dt.itemsize - 1)
+        payload = rng.integers(1, 1 << (mant - 1), k, dtype=np.uint64).astype(ut)
+        quiet = (rng.integers(0, 2, k).astype(ut) << ut.type(mant - 1))
+        bits[idx] = sign | exp | quiet | payload
     return x
 
 

@@ -213,3 +213,47 @@ def test_node_device_batch_rejects(aqz):
         assert "no HIP device" in str(e.value)
     finally:
         node.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [1, 0], [0, 1]], ids=["0,0", "1,0", "0,1"])
+def test_node_calls_leave_the_current_device(aqz, oracle, devices):
+    """Every node entry point restores the caller thread's current HIP device
+    (ADVICE r4): create, the stream calls, both batches and destroy, with the
+    caller on device 0 and handles on other devices where the box has them."""
+    torch = torch_cuda()
+    if max(devices) >= torch.cuda.device_count():
+        pytest.skip(f"needs {max(devices) + 1} GPUs")
+    torch.cuda.set_device(0)
+    geo = [(256, 128, 1), (128, 64, 1), (64, 32, 1)]
+    rng = np.random.default_rng(4)
+    frames = random_frames(rng, np.uint16, (4, 128, 256))
+
+    def here():
+        assert torch.cuda.current_device() == 0
+    node = aqz.Node(geo, np.uint16, aqz.MEAN, devices)
+    here()
+    try:
+        for f in frames[:2]:
+            node.add_frame(f)
+            here()
+            node.take_frame(1)
+            here()
+        node.flush()
+        here()
+        outs = [None] + [np.empty(2 * w * h * 2, np.uint8) for w, h, _ in geo[1:]]
+        node.run_host_batch(frames[2:].ctypes.data, 2, [0] + [o.ctypes.data for o in outs[1:]])
+        here()
+        d_in = to_device(frames)
+        d_outs = [None] + [empty_device(4 * w * h * 2) for w, h, _ in geo[1:]]
+        s = launch_stream()
+        counts = node.run_device_batch(d_in.data_ptr(), 0, 4,
+                                       [0] + [o.data_ptr() for o in d_outs[1:]], s)
+        here()
+        torch.cuda.synchronize()
+        assert counts == [4, 4, 4]
+        want = oracle.cascade_2d(frames[3], 3, aqz.MEAN)
+        got = d_outs[2][3 * 64 * 32 * 2:].cpu().numpy().view(np.uint16).reshape(32, 64)
+        assert np.array_equal(got, want[1])
+    finally:
+        node.close()
+    here()
