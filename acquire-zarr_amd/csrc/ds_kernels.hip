@@ -2154,12 +2154,14 @@ cascade_pick_cols(int dtype,
     // round 1, before band staging, had measured the opposite, 1083 -> 975
     // us for the wide tiles).  Rows that split lines keep the wide tiles and
     // their misaligned segments: 5472x3648 1091 against 1206 us narrow,
-    // 6000x4000 1049 against 1150, 2000^2 1085 against 1123.
+    // 6000x4000 1049 against 1150, 2000^2 1085 against 1123.  The same holds
+    // for the other 4- and 8-byte types at 4096^2: u32 Mean 994 -> 947 us,
+    // f64 Mean 1034 -> 884, f64 Max 1056 -> 889 (profiles/r05/widths/).
     // $AQZ_CASCADE_NARROW=0/1 (A/B) forces wide / narrow for 4- and 8-byte
     // types.
     static const int narrow_env = int_env("AQZ_CASCADE_NARROW", -1);
     const bool prefer_narrow = narrow_env >= 0 ? (narrow_env != 0 && b >= 4)
-                                               : (b == 4 && (uint64_t(W) * b) % 128 == 0);
+                                               : (b >= 4 && (uint64_t(W) * b) % 128 == 0);
     if (prefer_narrow && narrow)
         return cn;
     if (wide && W >= 64 * cw)
@@ -2505,14 +2507,14 @@ cascade_tiled_cols(int dtype, uint32_t W)
         return 0;
     const uint32_t cw = cascade_cols(b);
     // $AQZ_TILED_NARROW (A/B): 1 half-width tiles wherever they fit, 0 wide;
-    // unset: half-width for 4-byte types on line-aligned rows, as
+    // unset: half-width for 4- and 8-byte types on line-aligned rows, as
     // cascade_pick_cols (the streaming path writes a run tiled in one launch
     // only when both agree): chunk-tiled 4096^2 f32 964-979 against
     // 995-1033 us wide; 5472x3648, 6000x4000 and 2000^2 keep wide tiles
     // (1113 / 990 / 1031 against 1129 / 1074 / 1055 us narrow;
     // profiles/r05/narrow/ab_shapes.log)
     static const int narrow = int_env("AQZ_TILED_NARROW", -1);
-    if ((narrow == 1 || (narrow < 0 && b == 4 && (uint64_t(W) * b) % 128 == 0)) &&
+    if ((narrow == 1 || (narrow < 0 && b >= 4 && (uint64_t(W) * b) % 128 == 0)) &&
         W >= 64 * (cw / 2))
         return cw / 2;
     return W >= 64 * cw ? cw : cw / 2;

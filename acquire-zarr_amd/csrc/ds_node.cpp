@@ -790,99 +790,116 @@ aqz_node_run_device_batch(aqz_node* n,
         if ((e = hipEventRecord(ready, caller)) != hipSuccess)
             return hip_fail(n, e, "node_run_device_batch: event record");
 
-        const uint8_t* in = static_cast<const uint8_t*>(device_frames);
-        std::vector<hipEvent_t> joins;
-        int rc = AQZ_OK;
-        for (uint32_t d = 0; d < D && rc == AQZ_OK; ++d) {
-            const uint32_t u0 = first[d], nu = first[d + 1] - first[d];
-            if (nu == 0)
-                continue;
-            aqz_ds* h = n->ds[d];
-            const int dev = aqz_ds_device(h);
-            std::vector<void*> outs(nl, nullptr);
-            for (uint32_t L = 1; L < nl; ++L)
-                outs[L] = static_cast<uint8_t*>(device_out_levels[L]) + size_t(u0) * unit_bytes[L];
-            std::vector<uint32_t> cnt(nl, 0);
-            if (dev == src_device && !(flags & AQZ_NODE_STAGE_ALL)) {
-                // in place, on the caller's stream
-                rc = aqz_ds_run_device_batch(h, in + size_t(u0) * unit_bytes[0], nu * n->unit,
-                                             outs.data(), cnt.data(), caller);
-                if (rc)
-                    return fail(n, rc, "node_run_device_batch: handle " + std::to_string(d) +
-                                         ": " + aqz_ds_last_error(h));
+        // Everything queued so far drains before an error returns: blocks
+        // still read the caller's batch and write its outputs on the
+        // handles' streams, and the caller may free them on an error.
+        auto deal = [&]() -> int {
+            const uint8_t* in = static_cast<const uint8_t*>(device_frames);
+            std::vector<hipEvent_t> joins;
+            int rc = AQZ_OK;
+            for (uint32_t d = 0; d < D && rc == AQZ_OK; ++d) {
+                const uint32_t u0 = first[d], nu = first[d + 1] - first[d];
+                if (nu == 0)
+                    continue;
+                aqz_ds* h = n->ds[d];
+                const int dev = aqz_ds_device(h);
+                std::vector<void*> outs(nl, nullptr);
                 for (uint32_t L = 1; L < nl; ++L)
-                    if (cnt[L] != nu * n->per_unit[L])
-                        return fail(n, AQZ_INTERNAL_ERROR,
-                                    "node_run_device_batch: handle " + std::to_string(d) +
-                                      " emitted an unexpected frame count at level " +
-                                      std::to_string(L));
-                continue;
-            }
-            const uint32_t g_max = std::min(sub_units, nu);
-            if ((rc = peer_stage(n, d, src_device, size_t(g_max) * (unit_bytes[0] + unit_out))))
-                break;
-            PeerStage& p = n->peers[d];
-            if ((e = hipStreamWaitEvent(p.pull, ready, 0)) != hipSuccess)
-                return hip_fail(n, e, "node_run_device_batch: wait for the batch");
-            for (uint32_t j = 0; j < nu; j += g_max) {
-                const uint32_t g = std::min(g_max, nu - j);
-                const uint32_t s = p.next_slot;
-                p.next_slot ^= 1u;
-                uint8_t* slot = p.stage + size_t(s) * p.slot_bytes;
-                std::vector<void*> souts(nl, nullptr);
-                size_t off = size_t(g) * unit_bytes[0];
-                for (uint32_t L = 1; L < nl; ++L) {
-                    souts[L] = slot + off;
-                    off += size_t(g) * unit_bytes[L];
+                    outs[L] = static_cast<uint8_t*>(device_out_levels[L]) + size_t(u0) * unit_bytes[L];
+                std::vector<uint32_t> cnt(nl, 0);
+                if (dev == src_device && !(flags & AQZ_NODE_STAGE_ALL)) {
+                    // in place, on the caller's stream
+                    rc = aqz_ds_run_device_batch(h, in + size_t(u0) * unit_bytes[0], nu * n->unit,
+                                                 outs.data(), cnt.data(), caller);
+                    if (rc)
+                        return fail(n, rc, "node_run_device_batch: handle " + std::to_string(d) +
+                                             ": " + aqz_ds_last_error(h));
+                    for (uint32_t L = 1; L < nl; ++L)
+                        if (cnt[L] != nu * n->per_unit[L])
+                            return fail(n, AQZ_INTERNAL_ERROR,
+                                        "node_run_device_batch: handle " + std::to_string(d) +
+                                          " emitted an unexpected frame count at level " +
+                                          std::to_string(L));
+                    continue;
                 }
-                // pull: once the slot's previous pyramid has read its input
-                if ((e = hipStreamWaitEvent(p.pull, p.ran[s], 0)) != hipSuccess ||
-                    (e = hipMemcpyPeerAsync(slot, dev, in + size_t(u0 + j) * unit_bytes[0],
-                                            src_device, size_t(g) * unit_bytes[0], p.pull)) !=
-                      hipSuccess ||
-                    (e = hipEventRecord(p.pulled[s], p.pull)) != hipSuccess)
-                    return hip_fail(n, e, "node_run_device_batch: pull over xGMI");
-                // pyramid: once pulled and the slot's previous push has left
-                if ((e = hipStreamWaitEvent(p.run, p.pulled[s], 0)) != hipSuccess ||
-                    (e = hipStreamWaitEvent(p.run, p.pushed[s], 0)) != hipSuccess)
-                    return hip_fail(n, e, "node_run_device_batch: stream order");
-                rc = aqz_ds_run_device_batch(h, slot, g * n->unit, souts.data(), cnt.data(),
-                                             p.run);
-                if (rc)
-                    return fail(n, rc, "node_run_device_batch: handle " + std::to_string(d) +
-                                         ": " + aqz_ds_last_error(h));
-                for (uint32_t L = 1; L < nl; ++L)
-                    if (cnt[L] != g * n->per_unit[L])
-                        return fail(n, AQZ_INTERNAL_ERROR,
-                                    "node_run_device_batch: handle " + std::to_string(d) +
-                                      " emitted an unexpected frame count at level " +
-                                      std::to_string(L));
-                if ((e = hipSetDevice(dev)) != hipSuccess ||
-                    (e = hipEventRecord(p.ran[s], p.run)) != hipSuccess ||
-                    (e = hipStreamWaitEvent(p.push, p.ran[s], 0)) != hipSuccess)
-                    return hip_fail(n, e, "node_run_device_batch: stream order");
-                // push: each level to the block's place in the outputs
-                for (uint32_t L = 1; L < nl; ++L)
-                    if ((e = hipMemcpyPeerAsync(static_cast<uint8_t*>(outs[L]) +
-                                                  size_t(j) * unit_bytes[L],
-                                                src_device, souts[L], dev,
-                                                size_t(g) * unit_bytes[L], p.push)) != hipSuccess)
-                        return hip_fail(n, e, "node_run_device_batch: push over xGMI");
-                if ((e = hipEventRecord(p.pushed[s], p.push)) != hipSuccess)
+                const uint32_t g_max = std::min(sub_units, nu);
+                if ((rc = peer_stage(n, d, src_device, size_t(g_max) * (unit_bytes[0] + unit_out))))
+                    break;
+                PeerStage& p = n->peers[d];
+                if ((e = hipStreamWaitEvent(p.pull, ready, 0)) != hipSuccess)
+                    return hip_fail(n, e, "node_run_device_batch: wait for the batch");
+                for (uint32_t j = 0; j < nu; j += g_max) {
+                    const uint32_t g = std::min(g_max, nu - j);
+                    const uint32_t s = p.next_slot;
+                    p.next_slot ^= 1u;
+                    uint8_t* slot = p.stage + size_t(s) * p.slot_bytes;
+                    std::vector<void*> souts(nl, nullptr);
+                    size_t off = size_t(g) * unit_bytes[0];
+                    for (uint32_t L = 1; L < nl; ++L) {
+                        souts[L] = slot + off;
+                        off += size_t(g) * unit_bytes[L];
+                    }
+                    // pull: once the slot's previous pyramid has read its input
+                    if ((e = hipStreamWaitEvent(p.pull, p.ran[s], 0)) != hipSuccess ||
+                        (e = hipMemcpyPeerAsync(slot, dev, in + size_t(u0 + j) * unit_bytes[0],
+                                                src_device, size_t(g) * unit_bytes[0], p.pull)) !=
+                          hipSuccess ||
+                        (e = hipEventRecord(p.pulled[s], p.pull)) != hipSuccess)
+                        return hip_fail(n, e, "node_run_device_batch: pull over xGMI");
+                    // pyramid: once pulled and the slot's previous push has left
+                    if ((e = hipStreamWaitEvent(p.run, p.pulled[s], 0)) != hipSuccess ||
+                        (e = hipStreamWaitEvent(p.run, p.pushed[s], 0)) != hipSuccess)
+                        return hip_fail(n, e, "node_run_device_batch: stream order");
+                    rc = aqz_ds_run_device_batch(h, slot, g * n->unit, souts.data(), cnt.data(),
+                                                 p.run);
+                    if (rc)
+                        return fail(n, rc, "node_run_device_batch: handle " + std::to_string(d) +
+                                             ": " + aqz_ds_last_error(h));
+                    for (uint32_t L = 1; L < nl; ++L)
+                        if (cnt[L] != g * n->per_unit[L])
+                            return fail(n, AQZ_INTERNAL_ERROR,
+                                        "node_run_device_batch: handle " + std::to_string(d) +
+                                          " emitted an unexpected frame count at level " +
+                                          std::to_string(L));
+                    if ((e = hipSetDevice(dev)) != hipSuccess ||
+                        (e = hipEventRecord(p.ran[s], p.run)) != hipSuccess ||
+                        (e = hipStreamWaitEvent(p.push, p.ran[s], 0)) != hipSuccess)
+                        return hip_fail(n, e, "node_run_device_batch: stream order");
+                    // push: each level to the block's place in the outputs
+                    for (uint32_t L = 1; L < nl; ++L)
+                        if ((e = hipMemcpyPeerAsync(static_cast<uint8_t*>(outs[L]) +
+                                                      size_t(j) * unit_bytes[L],
+                                                    src_device, souts[L], dev,
+                                                    size_t(g) * unit_bytes[L], p.push)) != hipSuccess)
+                            return hip_fail(n, e, "node_run_device_batch: push over xGMI");
+                    if ((e = hipEventRecord(p.pushed[s], p.push)) != hipSuccess)
+                        return hip_fail(n, e, "node_run_device_batch: event record");
+                }
+                if ((e = hipEventRecord(p.done, p.push)) != hipSuccess)
                     return hip_fail(n, e, "node_run_device_batch: event record");
+                joins.push_back(p.done);
             }
-            if ((e = hipEventRecord(p.done, p.push)) != hipSuccess)
-                return hip_fail(n, e, "node_run_device_batch: event record");
-            joins.push_back(p.done);
-        }
-        if (rc)
+            if (rc)
+                return rc;
+            // the caller's stream owns the outputs again once every push is done
+            if ((e = hipSetDevice(src_device)) != hipSuccess)
+                return hip_fail(n, e, "node_run_device_batch: hipSetDevice");
+            for (hipEvent_t ev : joins)
+                if ((e = hipStreamWaitEvent(caller, ev, 0)) != hipSuccess)
+                    return hip_fail(n, e, "node_run_device_batch: join");
+            return AQZ_OK;
+        };
+        if (const int rc = deal(); rc != AQZ_OK) {
+            for (PeerStage& p : n->peers)
+                if (p.device >= 0) {
+                    (void)hipSetDevice(p.device);
+                    for (hipStream_t st : { p.pull, p.run, p.push })
+                        (void)hipStreamSynchronize(st);
+                }
+            (void)hipSetDevice(src_device);
+            (void)hipStreamSynchronize(caller);
             return rc;
-        // the caller's stream owns the outputs again once every push is done
-        if ((e = hipSetDevice(src_device)) != hipSuccess)
-            return hip_fail(n, e, "node_run_device_batch: hipSetDevice");
-        for (hipEvent_t ev : joins)
-            if ((e = hipStreamWaitEvent(caller, ev, 0)) != hipSuccess)
-                return hip_fail(n, e, "node_run_device_batch: join");
+        }
         if (out_counts) {
             out_counts[0] = n_frames;
             for (uint32_t L = 1; L < nl; ++L)

@@ -42,6 +42,9 @@ WORKLOADS = {
     "4096x4096_f32": (4096, 4096, 0, np.float32, 256, 0, 64),    # configs[3] (per GPU)
     "512x512_u8": (512, 512, 0, np.uint8, 128, 0, 1024),         # configs[0] synthetic
     "1024x1024x256_u16": (1024, 1024, 256, np.uint16, 256, 64, 256),  # configs[4]
+    # not BASELINE configs: the other element widths at the headline size
+    "4096x4096_u32": (4096, 4096, 0, np.uint32, 256, 0, 64),
+    "4096x4096_f64": (4096, 4096, 0, np.float64, 256, 0, 32),
 }
 HEADLINE_METRIC = "GPixels/s device-resident multiscale downsample, 4096² uint16, 5 levels"
 
@@ -321,8 +324,9 @@ def main():
     # synthetic input, resident in HBM before timing (seeded per rank)
     gen = torch.Generator(device="cuda").manual_seed(0xA0C2A11 + rank)
     if np.dtype(dtype).kind == "f":
-        d_in = (torch.rand(B * W * H, device="cuda", generator=gen) * 2000 - 1000
-                ).to(torch.float32).view(torch.uint8)
+        tdt = torch.float64 if np.dtype(dtype).itemsize == 8 else torch.float32
+        d_in = (torch.rand(B * W * H, device="cuda", generator=gen, dtype=tdt) * 2000 - 1000
+                ).view(torch.uint8)
     else:
         d_in = torch.randint(0, 256, (B * frame_bytes,), dtype=torch.uint8,
                              device="cuda", generator=gen)
