@@ -257,3 +257,40 @@ def test_node_calls_leave_the_current_device(aqz, oracle, devices):
     finally:
         node.close()
     here()
+
+
+def test_node_device_batch_staging_grows_between_calls(aqz, oracle):
+    """Staged blocks first in 1-unit sub-batches, then in one sub-batch of a
+    larger budget (the staging grows: its streams drain first), then small
+    again (the slots are reused as they are): three batches in a row equal
+    one oracle stream."""
+    torch = torch_cuda()
+    geo = [(384, 200, 1), (192, 100, 1), (96, 50, 1), (48, 25, 1)]
+    rng = np.random.default_rng(21)
+    sizes = [5, 9, 4]
+    frames = random_frames(rng, np.float32, (sum(sizes), 200, 384))
+    node = aqz.Node(geo, np.float32, aqz.MEAN, [0, 0, 0])
+    got = {L: [] for L in range(1, len(geo))}
+    try:
+        s = launch_stream()
+        k0 = 0
+        for nb, mb in zip(sizes, (1, 64, 1)):
+            d_in = to_device(frames[k0:k0 + nb])
+            outs = [None] + [empty_device(nb * w * h * 4) for w, h, _ in geo[1:]]
+            with stage_mb(mb):
+                c = node.run_device_batch(d_in.data_ptr(), 0, nb,
+                                          [0] + [o.data_ptr() for o in outs[1:]], s,
+                                          stage_all=True)
+            torch.cuda.synchronize()
+            assert c == [nb] * len(geo)
+            for L in got:
+                w, h, _ = geo[L]
+                got[L] += list(outs[L].cpu().numpy().view(np.float32).reshape(nb, h, w))
+            k0 += nb
+    finally:
+        node.close()
+    ref = oracle.OracleDownsampler(geo, np.float32, aqz.MEAN)
+    for k, f in enumerate(frames):
+        ref.add_frame(f)
+        for L in got:
+            assert_parity(got[L][k], ref.take_frame(L), f"frame {k} L{L}")
