@@ -2371,7 +2371,12 @@ aqz_method_metadata_json(int method)
 const char*
 aqz_version(void)
 {
-    return "aqz-mi355x 0.1.0 (gfx950)";
+    // AQZ_BUILD_ID: the source revision and time the Makefile built this
+    // library from, so a bench line names the binary it ran
+#ifndef AQZ_BUILD_ID
+#define AQZ_BUILD_ID "unknown build"
+#endif
+    return "aqz-mi355x 0.2.0 (gfx950; " AQZ_BUILD_ID ")";
 }
 
 } // extern "C"

@@ -713,6 +713,8 @@ def main():
                        "check": check},
             "comm_ms_per_step": (round(max(rank_comm_ms), 4) if xgmi else None),
             "xgmi_node": xgmi_node,
+            # the binary that ran: its source revision and build time
+            "library": aqz.lib().aqz_version().decode(),
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
             "e2e": e2e,
