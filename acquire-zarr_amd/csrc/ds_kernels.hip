@@ -2283,8 +2283,11 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // registers and the last wave only the shared ones (5-27% slower).
         static const int band_last_env = int_env("AQZ_BAND_LAST", -1);
         static const int mis_max_env = int_env("AQZ_BAND_MIS_MAX", -1);
+        // 16-byte tiles of 4-byte types move 1 KiB per row per wave, as the
+        // 2-byte tiles do, so they share the 2-byte thresholds
+        const bool tile16 = sizeof(T) == 2 || (sizeof(T) == 4 && cols == CN);
         const uint32_t mis_max = mis_max_env >= 0 ? uint32_t(std::min(mis_max_env, 8))
-                                                  : (sizeof(T) == 2 ? 6u : 4u);
+                                                  : (tile16 ? 6u : 4u);
         static const int mis_seg_env = std::min(int_env("AQZ_BAND_MIS_SEG", -1), 8);
         uint32_t stage_mask = 0;
         for (int i = 0; i < n_out; ++i) {
@@ -2360,7 +2363,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             band_waves = 8;
             wide_max = 8;
         } else if (misaligned && band_waves > mis_max && (sizeof(T) == 2 || sizeof(T) == 4) &&
-                   cols == CW && (mis_seg_env > 0 || (mis_seg_env < 0 && band_waves > 8))) {
+                   (cols == CW || tile16) &&
+                   (mis_seg_env > 0 || (mis_seg_env < 0 && band_waves > 8))) {
             // Misaligned bands of more than 8 tiles (2- and 4-byte types, wide
             // tiles): balanced segments of at most 4 tiles
             // ($AQZ_BAND_MIS_SEG: any band of those types wider than one
@@ -2444,7 +2448,8 @@ AQZ_SHARDED(launch_cascade)(int dtype,
                     // whole bands keep their code (a runtime branch per row
                     // cost 3000^2 / 2600^2 u16 8-9%), for 2- and 4-byte types
                     // at the wide tile only (where the launcher picks them)
-                    if constexpr ((sizeof(T) == 2 || sizeof(T) == 4) && C == int(CW)) {
+                    if constexpr ((sizeof(T) == 2 || sizeof(T) == 4) &&
+                                  (C == int(CW) || (sizeof(T) == 4 && C == int(CN)))) {
                         if (p.seg_rowwise) {
                             launch_band(std::true_type{}, std::false_type{});
                             return;
