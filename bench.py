@@ -178,6 +178,22 @@ def algorithmic_bytes(geo, counts, frames: int, method: str, bpp: int, tile=None
     return read, read + written
 
 
+class stdout_to_stderr:
+    """Send file descriptor 1 to stderr inside the block: gloo's C++ code
+    prints its connection messages ("[Gloo] Rank 0 is connected to ...") on
+    stdout, which must carry rank 0's JSON line alone."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def free_port() -> int:
     import socket
     s = socket.socket()
@@ -295,10 +311,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("AQZ_DIST_BACKEND", "nccl")  # nccl = RCCL
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend)
+        with stdout_to_stderr():
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            else:
+                dist.init_process_group(backend)
 
     W, H, Z, dtype, chunk, zchunk, default_batch = WORKLOADS[args.workload]
     if args.shape:
@@ -658,7 +675,8 @@ def main():
         # dealing host frames over all the ranks' GPUs, each over its own PCIe
         # link.  The other ranks wait on a CPU-only group meanwhile, so no
         # collective kernel spins on their GPUs.
-        cpu_group = dist.new_group(backend="gloo")
+        with stdout_to_stderr():
+            cpu_group = dist.new_group(backend="gloo")
         if rank == 0:
             n_vis = torch.cuda.device_count()
             # a gloo rehearsal on a smaller box repeats ordinals, as the ranks do
