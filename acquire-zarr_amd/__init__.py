@@ -803,6 +803,12 @@ class Node:
         finally:
             self._inflight.clear()
 
+    def wait_input(self):
+        """aqz_node_wait_input: every frame added so far is uploaded (the
+        caller may reuse its buffers); their levels may still be running."""
+        self._check(lib().aqz_node_wait_input(self._h))
+        self._inflight.clear()
+
     def __del__(self):
         self.close()
 

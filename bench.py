@@ -1476,6 +1476,33 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
         stream()
         el = time.perf_counter() - t0
         sbest = el if sbest is None else min(sbest, el)
+
+    # the drop-in's node mode (integration/src/streaming/downsampler.hip.cpp
+    # with $AQZ_GPU_DEVICES): one reused host buffer, as the frame queue
+    # hands frames over; per frame the next frame is copied in, added,
+    # waited for until uploaded (aqz_node_wait_input) and every ready level
+    # taken; a flush and a last drain at the end (MultiscaleArray::close_)
+    buf = np.empty_like(frames[0])
+
+    def dropin():
+        for f in frames:
+            np.copyto(buf, f)
+            node.add_frame(buf)
+            node.wait_input()
+            for L in levels:
+                while node.take_frame(L) is not None:
+                    pass
+        node.flush()
+        for L in levels:
+            while node.take_frame(L) is not None:
+                pass
+    dropin()  # warm
+    dbest = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        dropin()
+        el = time.perf_counter() - t0
+        dbest = el if dbest is None else min(dbest, el)
     node.close()
     in_bytes = n * W * H * bpp
     out_bytes = sum(o.numel() for o in outs[1:])
@@ -1484,6 +1511,10 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
             "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 1),
             "devices": list(devices), "shard_unit": node.unit,
             "stream_ms_per_frame": round(sbest / len(frames) * 1e3, 3),
+            "dropin_ms_per_frame": round(dbest / len(frames) * 1e3, 3),
+            "dropin_path": "one reused pageable buffer per frame: copy in, aqz_node_add_frame, "
+                           "aqz_node_wait_input, every ready level taken; flush at the end "
+                           "(the drop-in's $AQZ_GPU_DEVICES mode)",
             "stream_path": f"aqz_node_add_frame of {len(frames)} pageable frames, every level "
                            "taken when ready, then aqz_node_flush",
             "path": f"aqz_node_run_host_batch over handles on devices {list(devices)}, "
