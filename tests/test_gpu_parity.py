@@ -976,3 +976,46 @@ def test_bad_device_ordinal_is_invalid_argument(aqz):
     with pytest.raises(aqz.AqzError) as e:
         aqz.Downsampler(halving_geometry(64, 64, 2), np.uint8, aqz.MEAN, device=n_dev + 7)
     assert e.value.status == 1  # AQZ_INVALID_ARGUMENT
+
+
+# the oracle's NaN-rule KATs (tests/test_oracle_kats.py::test_mean_nan_payload_rule)
+# through the GPU: one 2x2 frame -> mean4, two 1x1 planes -> mean2
+_INF, _NINF, _ONE = 0x7F800000, 0xFF800000, 0x3F800000
+_QA, _QB, _SA = 0x7FC01234, 0xFFC0ABCD, 0x7F800F00
+NAN_KATS_4 = [
+    ([_QA, _QB, _ONE, _ONE], _QA),
+    ([_ONE, _QB, _QA, _ONE], _QB),
+    ([_SA, _ONE, _ONE, _ONE], _SA | 0x00400000),
+    ([_ONE, _SA, _QA, _ONE], _SA | 0x00400000),
+    ([_INF, _NINF, _ONE, _ONE], 0xFFC00000),
+    ([_INF, _NINF, _QA, _ONE], 0xFFC00000),
+    ([_ONE, _INF, _ONE, _NINF], 0xFFC00000),
+    ([_QB, _INF, _NINF, _ONE], _QB),
+]
+NAN_KATS_2 = [([_QA, _QB], _QA), ([_INF, _NINF], 0xFFC00000), ([_ONE, _SA], _SA | 0x00400000)]
+
+
+@pytest.mark.parametrize("bits,want", NAN_KATS_4)
+def test_mean4_nan_kats_gpu(aqz, bits, want):
+    frame = np.array(bits, dtype=np.uint32).view(np.float32).reshape(2, 2)
+    ds = aqz.Downsampler([(2, 2, 1), (1, 1, 1)], np.float32, aqz.MEAN)
+    try:
+        ds.add_frame(frame)
+        got = ds.take_frame(1)
+    finally:
+        ds.close()
+    assert int(got.view(np.uint32).reshape(-1)[0]) == want, hex(int(got.view(np.uint32)[0, 0]))
+
+
+@pytest.mark.parametrize("bits,want", NAN_KATS_2)
+def test_mean2_nan_kats_gpu(aqz, bits, want):
+    planes = np.array(bits, dtype=np.uint32).view(np.float32).reshape(2, 1, 1)
+    ds = aqz.Downsampler([(1, 1, 2), (1, 1, 1)], np.float32, aqz.MEAN)
+    try:
+        ds.add_frame(planes[0])
+        assert ds.take_frame(1) is None      # the earlier plane waits for its pair
+        ds.add_frame(planes[1])
+        got = ds.take_frame(1)
+    finally:
+        ds.close()
+    assert int(got.view(np.uint32).reshape(-1)[0]) == want, hex(int(got.view(np.uint32).reshape(-1)[0]))

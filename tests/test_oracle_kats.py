@@ -71,6 +71,50 @@ def test_compare_select_nan_order(oracle):
     assert oracle.reduce2(np.int16, oracle.DECIMATE, -5, 7) == -5
 
 
+def _mean_bits(oracle, ut, bits):
+    """The oracle's mean4 (4 operands) or mean2 (2) on raw bit patterns, so
+    no float conversion on the way quiets a signaling NaN."""
+    dt = np.float32 if ut is np.uint32 else np.float64
+    v = np.array(bits, dtype=ut).view(dt)
+    out = np.zeros(1, dtype=dt)
+    p, isz = v.ctypes.data, v.itemsize
+    code = oracle.dtype_code(dt)
+    if len(bits) == 4:
+        oracle.lib().oracle_reduce4(code, oracle.MEAN, p, p + isz, p + 2 * isz, p + 3 * isz,
+                                    out.ctypes.data)
+    else:
+        oracle.lib().oracle_reduce2(code, oracle.MEAN, p, p + isz, out.ctypes.data)
+    return int(out.view(ut)[0])
+
+
+def test_mean_nan_payload_rule(oracle):
+    """The reference binary's NaN result (x86 SSE addss/divss in the order
+    ((a + b) + c) + d, downsampler.cpp:48-51,108-112), which the GPU restates
+    (ds_kernels.hip x86_add): the first NaN operand wins, quieted; an invalid
+    sum (inf + -inf) gives the negative default NaN; a quiet NaN survives
+    the later adds and the divide.  Pinned against the reference itself by
+    tests/golden/reference_nan_vectors.npz (test_reference_pin.py)."""
+    inf, ninf, one = 0x7F800000, 0xFF800000, 0x3F800000
+    qa, qb = 0x7FC01234, 0xFFC0ABCD          # quiet, payloads, both signs
+    sa = 0x7F800F00                          # signaling (quiet bit clear)
+    u = np.uint32
+    assert _mean_bits(oracle, u, [qa, qb, one, one]) == qa          # first NaN
+    assert _mean_bits(oracle, u, [one, qb, qa, one]) == qb
+    assert _mean_bits(oracle, u, [sa, one, one, one]) == sa | 0x00400000  # quieted
+    assert _mean_bits(oracle, u, [one, sa, qa, one]) == sa | 0x00400000
+    assert _mean_bits(oracle, u, [inf, ninf, one, one]) == 0xFFC00000   # default NaN
+    assert _mean_bits(oracle, u, [inf, ninf, qa, one]) == 0xFFC00000   # made first
+    assert _mean_bits(oracle, u, [one, inf, one, ninf]) == 0xFFC00000
+    assert _mean_bits(oracle, u, [qb, inf, ninf, one]) == qb
+    assert _mean_bits(oracle, u, [qa, qb]) == qa                        # mean2
+    assert _mean_bits(oracle, u, [inf, ninf]) == 0xFFC00000
+    d = np.uint64
+    assert _mean_bits(oracle, d, [0x7FF0000000000001, 0x7FF8000000000002]) == \
+        0x7FF8000000000001
+    assert _mean_bits(oracle, d, [0x7FF0000000000000, 0xFFF0000000000000, 0, 0]) == \
+        0xFFF8000000000000
+
+
 @pytest.mark.parametrize("method", [0, 1, 2, 3])
 def test_2d_stream_expectations(oracle, method):
     """test_2d_multiscale_stream (test_stream.py:993-1077): int32 in
