@@ -2680,6 +2680,17 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
         p.zwaves = uint32_t(zw); // A/B only: 0 leaves the overhang unwritten
     p.remap = xcd_remap_env() == 1;
     p.nt = load_nt(W, b);
+    // Waves whose unit reads at most 4 KiB load plain, not nontemporal:
+    // chunk-tiled 512^2 u8 Decimate 74.0 -> 66.1 us and Mean 83.4 -> 74.8,
+    // 2048^2 u16 Decimate 72.6 -> 69.5; units that read 8 KiB or more keep
+    // the hint (4096^2 u16 Decimate 288 against 306 us plain, 2048^2 u16
+    // Mean 117 against 127, f32 Mean 986 against 1014; f32 Decimate ties)
+    // (same box, two rounds, profiles/r05/tilednt/ab.log).
+    if (load_nt_env() < 0) {
+        const uint64_t unit_read = (uint64_t(R) * 64u * cols * b) >> (method == kDecimate ? 1 : 0);
+        if (unit_read <= 4096)
+            p.nt = 0;
+    }
     // $AQZ_TILED_BAND_WG=1 (A/B, off by default): on rows that split 128-B
     // lines, one workgroup per row band (or balanced piece of <= 8 tiles), as
     // the row-major launcher does, so that the two waves sharing a line read
