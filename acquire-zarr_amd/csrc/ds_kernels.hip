@@ -2127,6 +2127,14 @@ cascade_fits(size_t b,
 #endif
 #if AQZ_SHARD == 0
 
+// 16-byte tiles for 4- and 8-byte types: rows whose level 1-4 rows are all
+// whole 64-B bursts (cascade_pick_cols, cascade_tiled_cols)
+static bool
+narrow_rows(size_t b, uint32_t W)
+{
+    return b >= 4 && (uint64_t(W) * b) % 1024 == 0;
+}
+
 uint32_t
 cascade_pick_cols(int dtype,
                   const void* src,
@@ -2157,11 +2165,15 @@ cascade_pick_cols(int dtype,
     // 6000x4000 1049 against 1150, 2000^2 1085 against 1123.  The same holds
     // for the other 4- and 8-byte types at 4096^2: u32 Mean 994 -> 947 us,
     // f64 Mean 1034 -> 884, f64 Max 1056 -> 889 (profiles/r05/widths/).
+    // "Whole lines" must hold for the levels too, not only level 0: f32
+    // 5472x3648 (21888-B rows, level 2 splits bursts) ran 1155 us narrow
+    // against 1065-1091 wide (profiles/r05/shapes/), so the rule asks for
+    // W * b a multiple of 1024 (levels 1-4 rows whole 64-B bursts).
     // $AQZ_CASCADE_NARROW=0/1 (A/B) forces wide / narrow for 4- and 8-byte
     // types.
     static const int narrow_env = int_env("AQZ_CASCADE_NARROW", -1);
     const bool prefer_narrow = narrow_env >= 0 ? (narrow_env != 0 && b >= 4)
-                                               : (b >= 4 && (uint64_t(W) * b) % 128 == 0);
+                                               : narrow_rows(b, W);
     if (prefer_narrow && narrow)
         return cn;
     if (wide && W >= 64 * cw)
@@ -2512,14 +2524,14 @@ cascade_tiled_cols(int dtype, uint32_t W)
         return 0;
     const uint32_t cw = cascade_cols(b);
     // $AQZ_TILED_NARROW (A/B): 1 half-width tiles wherever they fit, 0 wide;
-    // unset: half-width for 4- and 8-byte types on line-aligned rows, as
-    // cascade_pick_cols (the streaming path writes a run tiled in one launch
+    // unset: half-width for 4- and 8-byte types on rows whose levels are
+    // whole bursts (narrow_rows), as cascade_pick_cols (the streaming path writes a run tiled in one launch
     // only when both agree): chunk-tiled 4096^2 f32 964-979 against
     // 995-1033 us wide; 5472x3648, 6000x4000 and 2000^2 keep wide tiles
     // (1113 / 990 / 1031 against 1129 / 1074 / 1055 us narrow;
     // profiles/r05/narrow/ab_shapes.log)
     static const int narrow = int_env("AQZ_TILED_NARROW", -1);
-    if ((narrow == 1 || (narrow < 0 && b >= 4 && (uint64_t(W) * b) % 128 == 0)) &&
+    if ((narrow == 1 || (narrow < 0 && narrow_rows(b, W))) &&
         W >= 64 * (cw / 2))
         return cw / 2;
     return W >= 64 * cw ? cw : cw / 2;
