@@ -639,12 +639,13 @@ def main():
             e2e["pipelined"] = measure_e2e_pipelined(aqz, torch, geo, dtype, method,
                                                      d_in, min(B, 64), device)
             n_vis = torch.cuda.device_count()
-            e2e["node"] = measure_e2e_node(aqz, torch, geo, dtype, method, d_in, min(B, 64),
-                                           list(range(n_vis)) if n_vis > 1 else [device, device])
-            e2e["secondary_kernels"] = measure_secondary(aqz, torch, stream, d_in, W, H,
-                                                         dtype, chunk)
+            e2e["node"] = aux_leg("e2e.node", measure_e2e_node, aqz, torch, geo, dtype, method,
+                                  d_in, min(B, 64),
+                                  list(range(n_vis)) if n_vis > 1 else [device, device])
+            e2e["secondary_kernels"] = aux_leg("e2e.secondary_kernels", measure_secondary, aqz,
+                                               torch, stream, d_in, W, H, dtype, chunk)
             # §8(f) row 3 end to end: c-blosc frames of device chunks vs c-blosc
-            e2e["blosc_frames"] = measure_blosc_frames(aqz, torch)
+            e2e["blosc_frames"] = aux_leg("e2e.blosc_frames", measure_blosc_frames, aqz, torch)
             # BASELINE configs[1]: 2048^2 uint16, 4 levels, filesystem sink
             # (in a temporary directory, or under --sink)
             import tempfile
@@ -654,7 +655,8 @@ def main():
             if sink_root:
                 os.makedirs(sink_root, exist_ok=True)
             with tempfile.TemporaryDirectory(dir=sink_root) as tmp:
-                e2e["c2_filesystem_sink"] = measure_e2e_sink(
+                e2e["c2_filesystem_sink"] = aux_leg(
+                    "e2e.c2_filesystem_sink", measure_e2e_sink,
                     aqz, c2_geo, np.uint16, method, args.e2e_frames, device,
                     os.path.join(tmp, "c2"))
             if args.sink:
@@ -682,8 +684,11 @@ def main():
             # a gloo rehearsal on a smaller box repeats ordinals, as the ranks do
             rehearsal = n_vis < world and os.environ.get("AQZ_DIST_BACKEND") == "gloo"
             if n_vis >= world or rehearsal:
-                e2e["node"] = measure_e2e_node(aqz, torch, geo, dtype, method, d_in,
-                                               min(B, 64), [r % n_vis for r in range(world)])
+                # guarded: the other ranks wait at the barrier below, so an
+                # exception here must not leave rank 0 without reaching it
+                e2e["node"] = aux_leg("e2e.node", measure_e2e_node, aqz, torch, geo, dtype,
+                                      method, d_in, min(B, 64),
+                                      [r % n_vis for r in range(world)])
                 if rehearsal:
                     e2e["node"]["rehearsal"] = f"{world} handles on {n_vis} device(s)"
             else:
@@ -1429,6 +1434,20 @@ def measure_e2e_pipelined(aqz, torch, geo, dtype, method, d_in, n, device, dist=
             "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 1),
             "path": "aqz_ds_run_host_batch, pinned host in/out, "
                     f"{n} frames, H2D/kernels/D2H overlapped"}
+
+
+def aux_leg(name, fn, *args, **kwargs):
+    """Run one auxiliary measurement (an `e2e` sub-leg, after the timed
+    region and the oracle check).  A failure there is reported in the line
+    as {"error": ...}, with its traceback on stderr, rather than losing the
+    line or, at N > 1, leaving the other ranks waiting at a barrier."""
+    try:
+        return fn(*args, **kwargs)
+    except Exception as e:  # reported, never silent
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        print(f"bench: {name} failed: {type(e).__name__}: {e}", file=sys.stderr)
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):

@@ -76,3 +76,15 @@ def test_under_launcher_world_size_wins():
     assert bench.resolve_world(bench.parse([]), env) == ("run", 4)
     with pytest.raises(SystemExit):
         bench.resolve_world(bench.parse(["--gpus", "8"]), env)
+
+
+def test_aux_leg_reports_a_failure_in_the_line(capsys):
+    # an auxiliary e2e leg that raises leaves {"error": ...} in the line (and
+    # its traceback on stderr) instead of losing the line or stranding ranks
+    assert bench.aux_leg("ok", lambda a, b=0: {"v": a + b}, 1, b=2) == {"v": 3}
+
+    def boom():
+        raise RuntimeError("hipErrorPeerAccessUnsupported")
+    out = bench.aux_leg("e2e.node", boom)
+    assert out == {"error": "RuntimeError: hipErrorPeerAccessUnsupported"}
+    assert "e2e.node failed" in capsys.readouterr().err
