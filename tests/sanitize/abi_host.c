@@ -135,6 +135,15 @@ main(void)
         int done = 0;
         if (aqz_ds_poll(NULL, &done) != AQZ_INVALID_ARGUMENT)
             return 29;
+        /* round-5 entry points: NULL handles refused, nothing touched */
+        uint32_t counts[3] = { 0 };
+        void* outs[3] = { NULL, NULL, NULL };
+        if (aqz_node_run_device_batch(NULL, devs, 0, 4, outs, counts, NULL, 0) !=
+              AQZ_INVALID_ARGUMENT ||
+            aqz_node_set_level_tiling(NULL, 1, 16, 16) != AQZ_INVALID_ARGUMENT ||
+            aqz_node_wait_input(NULL) != AQZ_INVALID_ARGUMENT ||
+            aqz_ds_wait_input(NULL) != AQZ_INVALID_ARGUMENT)
+            return 30;
     }
     printf("abi_host: ok (%s; %s)\n", aqz_version(), aqz_blosc_codec_info());
     return 0;
