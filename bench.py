@@ -642,6 +642,11 @@ def main():
             e2e["node"] = aux_leg("e2e.node", measure_e2e_node, aqz, torch, geo, dtype, method,
                                   d_in, min(B, 64),
                                   list(range(n_vis)) if n_vis > 1 else [device, device])
+            if not args.tiled:
+                e2e["node_device_batch"] = aux_leg(
+                    "e2e.node_device_batch", measure_node_device_batch, aqz, torch, geo, dtype,
+                    method, d_in, outs, counts, B, frame_bytes, device,
+                    list(range(n_vis)) if n_vis > 1 else [device, device], stream, avg_launch_s)
             e2e["secondary_kernels"] = aux_leg("e2e.secondary_kernels", measure_secondary, aqz,
                                                torch, stream, d_in, W, H, dtype, chunk)
             # §8(f) row 3 end to end: c-blosc frames of device chunks vs c-blosc
@@ -689,6 +694,13 @@ def main():
                 e2e["node"] = aux_leg("e2e.node", measure_e2e_node, aqz, torch, geo, dtype,
                                       method, d_in, min(B, 64),
                                       [r % n_vis for r in range(world)])
+                if not args.tiled:
+                    # config F's shape of work: rank 0's device-resident batch
+                    # dealt over every rank's GPU by peer copies (xGMI)
+                    e2e["node_device_batch"] = aux_leg(
+                        "e2e.node_device_batch", measure_node_device_batch, aqz, torch, geo,
+                        dtype, method, d_in, outs, counts, B, frame_bytes, device,
+                        [r % n_vis for r in range(world)], stream, avg_launch_s)
                 if rehearsal:
                     e2e["node"]["rehearsal"] = f"{world} handles on {n_vis} device(s)"
             else:
@@ -1448,6 +1460,66 @@ def aux_leg(name, fn, *args, **kwargs):
         traceback.print_exc(file=sys.stderr)
         print(f"bench: {name} failed: {type(e).__name__}: {e}", file=sys.stderr)
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+def measure_node_device_batch(aqz, torch, geo, dtype, method, d_in, outs, counts, B,
+                              frame_bytes, device, devices, stream, local_launch_s, reps=5):
+    """BASELINE config F's multi-GPU form through the library
+    (aqz_node_run_device_batch): len(devices) copies of this
+    rank's device-resident batch, on this GPU, dealt over `devices` in whole
+    shard units; remote blocks are pulled and their levels pushed back by
+    hipMemcpyPeerAsync (xGMI DMA), levels land in frame order.  Every block's
+    levels are compared with this rank's own batch (`outs`, the timed
+    kernel's output of the same frames).  The rate is set against the timed
+    kernel: one GPU would take len(devices) x its launch time."""
+    ND = len(devices)
+    pool = torch.empty(ND * B * frame_bytes, dtype=torch.uint8, device="cuda")
+    for r in range(ND):
+        pool[r * B * frame_bytes:(r + 1) * B * frame_bytes].copy_(d_in[:B * frame_bytes])
+    levels = [None] + [torch.empty(ND * o.numel(), dtype=torch.uint8, device="cuda")
+                       for o in outs[1:]]
+    torch.cuda.synchronize()
+    node = aqz.Node(geo, dtype, method, devices)
+    try:
+        call = node.device_batch_call(pool.data_ptr(), device, ND * B,
+                                      [0] + [t.data_ptr() for t in levels[1:]],
+                                      stream.cuda_stream)
+        got = call()  # warm: staging and streams on the remote GPUs
+        torch.cuda.synchronize()
+        exact = True
+        for L in range(1, len(geo)):
+            w, h, _ = geo[L]
+            nb = counts[L] * w * h * np.dtype(dtype).itemsize
+            exact = exact and got[L] == ND * counts[L]
+            for r in range(ND):
+                exact = exact and bool(torch.equal(levels[L][r * outs[L].numel():
+                                                             r * outs[L].numel() + nb],
+                                                   outs[L][:nb]))
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record(stream)
+        for _ in range(reps):
+            call()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / reps
+    finally:
+        node.close()
+    W, H, _ = geo[0]
+    one_gpu_ms = ND * local_launch_s * 1e3
+    out = {"value": round(ND * B * W * H / (ms * 1e-3) / 1e9, 3), "unit": "GPixels/s",
+           "ms_per_call": round(ms, 4), "frames_per_call": ND * B, "devices": list(devices),
+           "one_gpu_ms_same_frames": round(one_gpu_ms, 4),
+           "speedup_vs_one_gpu": round(one_gpu_ms / ms, 3),
+           "check": ("bit-exact" if exact else "MISMATCH") +
+                    f" (all {ND} blocks vs this rank's own batch)",
+           "path": "aqz_node_run_device_batch: this GPU's batch dealt in whole shard units, "
+                   "remote blocks pulled and levels pushed by hipMemcpyPeerAsync (xGMI DMA) "
+                   "through two staging slots per GPU, levels in frame order"}
+    if len(set(devices)) < len(devices):
+        out["rehearsal"] = (f"{len(devices)} handles on {len(set(devices))} device(s): "
+                            "blocks on the batch's own GPU run in place, one after "
+                            "another, so no speed-up is possible")
+    return out
 
 
 def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
