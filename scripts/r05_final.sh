@@ -20,6 +20,7 @@ python -c "import json;d=json.load(open('$OUT/bench_headline.json'));r=d['roofli
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
   python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 --e2e-frames 0 --no-check --no-pmc > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
 find $OUT/prof -name "*kernel_stats*" | head -3
+[ "${METHODS:-1}" = 1 ] || { echo "== done (no method sweep)"; exit 0; }
 for w in 4096x4096_u16 4096x4096_f32 1024x1024x256_u16 2048x2048_u16 512x512_u8; do
   for m in decimate mean min max; do
     timeout -k 10 300 python bench.py --workload $w --method $m --steps 20 --warmup 5 --cpu-seconds 0 \
