@@ -1599,9 +1599,11 @@ volume_coords(const VolumeParams& p, uint32_t u, int lane, uint32_t& g, uint32_t
 // NTL: nontemporal loads.  UPW units per wave (consecutive, columns first):
 // with UPW > 1 and every unit inside the frame, all of them are loaded
 // before the first is reduced, so a wave has UPW units' loads in flight —
-// Decimate's units read only 4 KiB.  Round 5: Decimate's
-// volume launch ran at 0.64 of spec with nontemporal loads and 0.82-0.86
-// with plain ones (tools/volume_probe.hip).
+// Decimate's units read only 4 KiB.  Round 5: with the
+// volume in HBM, Decimate's launch runs at 0.59-0.60 of spec with
+// nontemporal loads and 0.55-0.56 with plain ones; the 0.82 once measured
+// with plain loads came from the Infinity Cache holding the launch's
+// 128 MiB read set between launches.
 template<typename T, int M, int NL, bool NTL, int UPW, int C = 16 / int(sizeof(T)),
          bool ZFAST = false>
 __global__ __launch_bounds__(256) void
@@ -2239,22 +2241,31 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         // 4 waves per block, one tile per wave per iteration.
         static const uint32_t wpb = uint32_t(std::clamp(int_env("AQZ_CASCADE_WAVES", 4), 1, 8));
         static const uint32_t order = uint32_t(std::clamp(int_env("AQZ_UNIT_ORDER", 0), 0, 2));
-        // Units per wave (cascade_kernel's loop): a wave whose unit reads
-        // under 4 KiB takes 2, 4 or 8 consecutive units, so that it moves at
-        // least that much.  512^2 u8 (2 KiB units; Decimate reads half of
-        // each): Decimate 57.8 -> 39.4 us with 4, Mean 61.5 -> 56.9 and Max
-        // 63.9 -> 57.7 with 2 (4 lost against 2); 2048^2 u16 Decimate (4 KiB
-        // units) lost with 2 (69.1 -> 71.7), so it keeps 1; same box, two
-        // rounds (profiles/r04/upw/).  $AQZ_UNITS_PER_WAVE=k forces k.
+        // Units per wave (cascade_kernel's loop): a Decimate wave whose unit
+        // reads under 4 KiB takes 2, 4 or 8 consecutive units, so that it
+        // moves at least that much: 512^2 u8 Decimate (1 KiB read per unit)
+        // 55.3 -> 40.7 us with 4 (8: 45.8).  Other methods keep one unit per
+        // wave and, where that unit is under 4 KiB, load plain: 512^2 u8
+        // Mean 61.4-62.0 -> 59.4-59.8 us, Max 61.8 -> 60.6-61.2 against two
+        // units with nontemporal loads.  Round 5, with the input and output
+        // in HBM (rotating buffer sets); round 4's
+        // two-unit Mean/Max choice had been timed with the whole read set
+        // resident in the Infinity Cache.  2048^2 u16 Decimate (4 KiB units)
+        // keeps 1 (two: 76.5 -> 78.8-80.1 us).  $AQZ_UNITS_PER_WAVE=k forces k.
         static const int upw_env = int_env("AQZ_UNITS_PER_WAVE", 0);
         uint32_t upw = 1;
+        bool small_plain = false;
         if (upw_env > 0) {
             upw = uint32_t(std::min(upw_env, 16));
         } else {
             const uint64_t unit_bytes = (uint64_t(R) * 64u * cols * sizeof(T)) >>
                                         (method == kDecimate ? 1 : 0);
-            while (upw < 8 && unit_bytes * upw < 4096)
-                upw *= 2;
+            if (method == kDecimate) {
+                while (upw < 8 && unit_bytes * upw < 4096)
+                    upw *= 2;
+            } else {
+                small_plain = unit_bytes < 4096;
+            }
         }
         p.upw = order == 0 ? upw : 1u;
         const uint32_t grid = grid_for((total + p.upw - 1) / p.upw, wpb, 0);
@@ -2263,15 +2274,12 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         p.remap = xcd_remap_env() == 1;
         p.wb = store_wb_env() >= 0 ? uint32_t(store_wb_env()) : 0u;
         p.nt = load_nt(W, sizeof(T));
-        // Decimate waves that loop over small units (half of each unit's rows
-        // read) load plain, not nontemporal: 512^2 u8 Decimate (4 units per
-        // wave) 37.0 -> 33.7 us, 0.89 -> 0.99 of the same-mix ceiling, as the
-        // volume Decimate (launch_volume).  Everything else measured keeps
-        // the nontemporal hint on aligned rows: 4096^2 u16 / f32 and 2048^2
-        // u16 Decimate (one 4-KiB unit per wave) 290 / 605 / 67.6 us with it
-        // against 306 / 653 / 80.3 without, Mean 5-20% slower without it
-        // (profiles/r05/decnt/ab.log).
-        if (load_nt_env() < 0 && method == kDecimate && p.upw > 1)
+        // Loads keep the nontemporal hint on aligned rows, Decimate's looped
+        // small units included (512^2 u8 Decimate 40.7 us against 42.1-42.5
+        // plain, with the data in HBM; the round-5 plain-load rule had been
+        // timed with its 128 MiB read set resident in the Infinity Cache,
+        // DESIGN.md §11.11), except the small single units above.
+        if (load_nt_env() < 0 && small_plain)
             p.nt = 0;
         // Band staging when some level's rows are not whole 64-byte bursts
         // and a row band is at most 4 tiles, 6 for 2-byte types
@@ -2691,18 +2699,13 @@ AQZ_SHARDED(launch_cascade_tiled)(int dtype,
     if (const int zw = tiled_zwaves_env(); zw >= 0)
         p.zwaves = uint32_t(zw); // A/B only: 0 leaves the overhang unwritten
     p.remap = xcd_remap_env() == 1;
+    // Nontemporal loads on aligned rows for every unit size: with the data
+    // in HBM (rotating buffer sets) chunk-tiled 2048^2
+    // u16 Decimate runs 73.8-73.9 us with them against 79.0-79.7 plain, and
+    // 512^2 u8 Decimate / Mean 73.1-73.5 / 82.6-82.7 against 74.1 / 83.4-
+    // 84.8.  (A round-5 plain-load rule for units of <= 4 KiB had been timed
+    // with the read set resident in the Infinity Cache.)
     p.nt = load_nt(W, b);
-    // Waves whose unit reads at most 4 KiB load plain, not nontemporal:
-    // chunk-tiled 512^2 u8 Decimate 74.0 -> 66.1 us and Mean 83.4 -> 74.8,
-    // 2048^2 u16 Decimate 72.6 -> 69.5; units that read 8 KiB or more keep
-    // the hint (4096^2 u16 Decimate 288 against 306 us plain, 2048^2 u16
-    // Mean 117 against 127, f32 Mean 986 against 1014; f32 Decimate ties)
-    // (same box, two rounds, profiles/r05/tilednt/ab.log).
-    if (load_nt_env() < 0) {
-        const uint64_t unit_read = (uint64_t(R) * 64u * cols * b) >> (method == kDecimate ? 1 : 0);
-        if (unit_read <= 4096)
-            p.nt = 0;
-    }
     // $AQZ_TILED_BAND_WG=1 (A/B, off by default): on rows that split 128-B
     // lines, one workgroup per row band (or balanced piece of <= 8 tiles), as
     // the row-major launcher does, so that the two waves sharing a line read
@@ -2837,15 +2840,19 @@ AQZ_SHARDED(launch_volume)(int dtype,
             p.w[i] = outs[i].w;
             p.h[i] = outs[i].h;
         }
-        // Load policy and units per wave: Decimate's
-        // every-other-row, every-other-plane reads run 25% faster with plain
-        // loads than nontemporal ones, and its 4-KiB units two to a wave;
-        // $AQZ_VOLUME_NT=0/1 and $AQZ_VOLUME_UPW=1/2 (Decimate) override.
+        // Load policy and units per wave: with the
+        // volume in HBM (rotating buffer sets) nontemporal loads beat plain
+        // ones for every method, Decimate's every-other-row, every-other-
+        // plane reads included (44.0-44.4 against 46.7-47.4 us); Decimate's
+        // 4-KiB units go two to a wave (one ties).  The plain-load choice of
+        // §11.2 had been timed with Decimate's 128 MiB read set resident in
+        // the Infinity Cache.  $AQZ_VOLUME_NT=0/1 and $AQZ_VOLUME_UPW=1/2
+        // (Decimate) override.
         static const int nt_env = int_env("AQZ_VOLUME_NT", -1);
         static const int upw_env = int_env("AQZ_VOLUME_UPW", 0);
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
-            const bool ntl = nt_env >= 0 ? nt_env != 0 : M != kDecimate;
+            const bool ntl = nt_env >= 0 ? nt_env != 0 : true;
             const int upw = M == kDecimate ? (upw_env > 0 ? std::min(upw_env, 2) : 2) : 1;
             const uint32_t grid = grid_for((total + upw - 1) / upw, 4, 0);
 #define AQZ_VOL(NL, NTL, UPW)                                                          \

@@ -241,6 +241,12 @@ def parse(argv=None):
     p.add_argument("--batch", type=int, default=0,
                    help="frames (planes) per step per GPU; 0 = workload default")
     p.add_argument("--method", default="mean", choices=["decimate", "mean", "min", "max"])
+    p.add_argument("--rotate-mib", type=int, default=1024,
+                   help="launches cycle over copies of the input and output buffers "
+                        "until the bytes a launch reads, over all copies, reach this "
+                        "many MiB (4x the 256 MB Infinity Cache by default), so that "
+                        "no launch finds its input left in the cache by the launch "
+                        "before; 0: one buffer set")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--e2e-frames", type=int, default=48,
@@ -340,16 +346,24 @@ def main():
     bpp = np.dtype(dtype).itemsize
     B = args.batch or default_batch
     frame_bytes = W * H * bpp
+    n_rot = rotation_copies(B * frame_bytes, args.method, bool(Z), args.rotate_mib)
+    if args.xgmi_scatter or args.xgmi_rccl:
+        n_rot = 1  # these modes keep one buffer set (their batches are >= 2 GiB)
 
-    # synthetic input, resident in HBM before timing (seeded per rank)
+    # synthetic input, resident in HBM before timing (seeded per rank);
+    # n_rot copies of it at distinct addresses (copy 0 is `d_in`)
     gen = torch.Generator(device="cuda").manual_seed(0xA0C2A11 + rank)
+    d_all = torch.empty(n_rot * B * frame_bytes, dtype=torch.uint8, device="cuda")
+    d_in = d_all[:B * frame_bytes]
     if np.dtype(dtype).kind == "f":
         tdt = torch.float64 if np.dtype(dtype).itemsize == 8 else torch.float32
-        d_in = (torch.rand(B * W * H, device="cuda", generator=gen, dtype=tdt) * 2000 - 1000
-                ).view(torch.uint8)
+        d_in.view(tdt).copy_(torch.rand(B * W * H, device="cuda", generator=gen, dtype=tdt)
+                             * 2000 - 1000)
     else:
-        d_in = torch.randint(0, 256, (B * frame_bytes,), dtype=torch.uint8,
-                             device="cuda", generator=gen)
+        d_in.copy_(torch.randint(0, 256, (B * frame_bytes,), dtype=torch.uint8,
+                                 device="cuda", generator=gen))
+    for k in range(1, n_rot):
+        d_all[k * B * frame_bytes:(k + 1) * B * frame_bytes].copy_(d_in)
     ds = aqz.Downsampler(geo, dtype, method, device=device)
     if args.tiled:
         # chunk x chunk tiles per level, zero overhang included
@@ -366,6 +380,10 @@ def main():
         outs = [None] + [torch.empty(B * w * h * bpp, dtype=torch.uint8, device="cuda")
                          for w, h, _ in geo[1:]]
     out_ptrs = [0] + [o.data_ptr() for o in outs[1:]]
+    # output sets of the other copies (set 0 is `outs`, the checked one)
+    rot_outs = [[None] + [torch.empty_like(o) for o in outs[1:]] for _ in range(1, n_rot)]
+    rot_flags = ([[None] + [torch.empty_like(f) for f in flags[1:]] for _ in range(1, n_rot)]
+                 if args.tiled and flag_ptrs is not None else None)
     # A real (non-null) stream: the kernels run on it and the timing events
     # are recorded on it.
     torch.cuda.synchronize()  # inputs were generated on the default stream
@@ -418,6 +436,18 @@ def main():
                               device_nonzero=flag_ptrs)
     else:
         batch = ds.batch_call(d_in.data_ptr(), B, out_ptrs, sptr)
+    # one call per buffer copy; steps take them in turn (copy 0 first)
+    def copy_call(k):
+        src = d_all.data_ptr() + k * B * frame_bytes
+        ptrs = [0] + [o.data_ptr() for o in rot_outs[k - 1][1:]]
+        if not args.tiled:
+            return ds.batch_call(src, B, ptrs, sptr)
+        return ds.batch_call(src, B, ptrs, sptr,
+                             tiles=[None] + [(chunk, chunk)] * (n_levels - 1),
+                             device_nonzero=(None if rot_flags is None else
+                                             [0] + [f.data_ptr() for f in rot_flags[k - 1][1:]]))
+    batches = [batch] + [copy_call(k) for k in range(1, n_rot)]
+    turn = [0]
 
     def step(ev=None):
         """One step; `ev` = (start, kernel_start, kernel_end, end) events
@@ -447,7 +477,8 @@ def main():
         else:
             if ev:
                 ev[1].record(stream)
-            counts[:] = batch()
+            counts[:] = batches[turn[0] % n_rot]()
+            turn[0] += 1
             if ev:
                 ev[2].record(stream)
 
@@ -462,6 +493,7 @@ def main():
     # correctness spot check of one frame against the oracle (rank 0, N=1)
     check = None
     if not args.no_check:
+        turn[0] = 0  # the checked outputs are copy 0's
         step()  # every rank: in --xgmi-scatter mode the step is collective
         torch.cuda.synchronize()
     if not args.no_check and rank == 0:
@@ -600,7 +632,28 @@ def main():
                 "min_launch_us": round(min(launch_ms) * 1e3, 2) if per_launch else None,
                 "launch_timing": ("HIP event pair around every launch" if per_launch else
                                   f"HIP events around the {args.steps} back-to-back launches "
-                                  "of the timed region, on the launch stream")}
+                                  "of the timed region, on the launch stream"),
+                "buffer_sets": n_rot}
+    if n_rot > 1:
+        # the same launches on one buffer set, for contrast: what the cache
+        # keeps of a read set this small shows up here, not in `frac`
+        kev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda.synchronize()
+        for _ in range(3):
+            batches[0]()
+        kev[0].record(stream)
+        for _ in range(args.steps):
+            batches[0]()
+        kev[1].record(stream)
+        torch.cuda.synchronize()
+        one_us = kev[0].elapsed_time(kev[1]) / args.steps * 1e3
+        roofline["buffer_rotation"] = {
+            "copies": n_rot, "bytes_per_copy": B * frame_bytes,
+            "why": (f"a launch reads {read_bytes} B; {n_rot} input/output copies in turn "
+                    f"keep {n_rot * read_bytes} B of reads between reuses, so the "
+                    "256 MB Infinity Cache cannot serve a launch from the one before"),
+            "one_buffer_set_avg_launch_us": round(one_us, 2),
+            "one_buffer_set_frac": round(alg_bytes / (one_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
     if world > 1:
         # kernel-only fractions: in --xgmi-scatter mode the p2p time is
@@ -612,8 +665,8 @@ def main():
             for r, c in enumerate(rank_comm_ms):
                 roofline["per_rank"][r]["comm_ms_per_step"] = round(c, 4)
 
-    ceiling = measure_ceiling(torch, stream, d_in, read_bytes, alg_bytes - read_bytes,
-                              max(5, args.steps // 2))
+    ceiling = measure_ceiling(torch, stream, d_all, read_bytes, alg_bytes - read_bytes,
+                              max(5, args.steps // 2), n_rot, B * frame_bytes)
     if ceiling is not None:
         ceiling["frac_of_ceiling"] = round(achieved / ceiling["GBps"], 4)
         roofline["same_mix_ceiling"] = ceiling
@@ -933,7 +986,21 @@ def measure_blosc_frames(aqz, torch, threads=16, n_chunks=256, reps=5):
             "cblosc_version": blosc_ref.version()}
 
 
-def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
+def rotation_copies(in_bytes: int, method: str, volume: bool, rotate_mib: int) -> int:
+    """Buffer sets the timed launches take in turn: enough that the bytes a
+    launch reads (Decimate reads every other row, and for volumes every
+    other plane too), summed over the sets, reach `rotate_mib` MiB.  Round 5
+    (DESIGN.md §11.11): volume Decimate reads 128 MiB per launch, which the
+    256 MB Infinity Cache held from one launch to the next; at four volumes
+    per launch the same kernel ran 30% slower per volume."""
+    if rotate_mib <= 0 or in_bytes <= 0:
+        return 1
+    read = in_bytes // (4 if volume else 2) if method == "decimate" else in_bytes
+    return max(1, min(64, -(-(rotate_mib << 20) // max(1, read))))
+
+
+def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps, n_rot=1,
+                    copy_bytes=0):
     """Measured HBM ceiling for the kernel's own byte mix (tools/hbm_probe.hip):
     a contiguous stream reading the same input buffer and writing (non-
     temporal stores) in the nearest of the ratios 12:4, 13:3, 14:2, 10:6, 9:7
@@ -941,8 +1008,10 @@ def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
     on the launch stream.  Round 5: each pass runs with nontemporal and with
     plain loads and the faster counts (plain loads beat nontemporal ones on
     the volume Decimate launch), so the ceiling is the best
-    of both policies.  A measurement aid, not product code: skipped (None) if
-    the probe library was not built."""
+    of both policies.  With `n_rot` buffer sets (rotation_copies) the passes
+    take the input copies `copy_bytes` apart and as many output regions in
+    turn, as the timed launches do.  A measurement aid, not product code:
+    skipped (None) if the probe library was not built."""
     import ctypes
     path = os.path.join(ROOT, "tools", "libaqz_hbm_probe.so")
     if not os.path.exists(path):
@@ -954,16 +1023,21 @@ def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     frac_r = read_bytes / max(1, read_bytes + write_bytes)
     rd, wr = min(((12, 4), (13, 3), (14, 2), (10, 6), (9, 7)), key=lambda m: abs(m[0] / 16 - frac_r))
-    dst = torch.empty(read_bytes // rd * wr + 4096, dtype=torch.uint8, device="cuda")
+    dst_bytes = (read_bytes // rd * wr + 4096 + 4095) // 4096 * 4096
+    dst = torch.empty(n_rot * dst_bytes, dtype=torch.uint8, device="cuda")
     sink = torch.zeros(16, dtype=torch.uint8, device="cuda")
     out = {}
     for name, (r, w) in (("GBps", (rd, wr)), ("read_only_GBps", (16, 0))):
         best = {}
         for nt in (1, 0):
             moved = ctypes.c_uint64(0)
+            turn = [0]
 
             def go():
-                rc = lib.aqz_hbm_probe_ld(d_in.data_ptr(), read_bytes, dst.data_ptr(),
+                k = turn[0] % n_rot
+                turn[0] += 1
+                rc = lib.aqz_hbm_probe_ld(d_in.data_ptr() + k * copy_bytes, read_bytes,
+                                          dst.data_ptr() + k * dst_bytes,
                                           sink.data_ptr(), r, w, nt, stream.cuda_stream,
                                           ctypes.byref(moved))
                 if rc != 0:
@@ -982,6 +1056,7 @@ def measure_ceiling(torch, stream, d_in, read_bytes, write_bytes, reps):
         out[name] = max(best.values())
         out[name + "_by_load"] = best
     out["read_write"] = f"{rd}:{wr}"
+    out["buffer_sets"] = n_rot
     out["kernel"] = ("tools/hbm_probe.hip: contiguous loads (best of nt and plain) and nt "
                      "stores, one 4 KiB-block round per workgroup, same input buffer and "
                      "stream")
@@ -1009,7 +1084,8 @@ def measure_traffic(args, kernel):
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
                "--workload", args.workload, "--batch", str(args.batch),
-               "--method", args.method, "--steps", "3", "--warmup", "1", "--no-check"]
+               "--method", args.method, "--steps", "3", "--warmup", "1", "--no-check",
+               "--rotate-mib", str(args.rotate_mib)]
         if args.tiled:
             cmd.append("--tiled")
         if args.no_flags:

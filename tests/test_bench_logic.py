@@ -88,3 +88,23 @@ def test_aux_leg_reports_a_failure_in_the_line(capsys):
     out = bench.aux_leg("e2e.node", boom)
     assert out == {"error": "RuntimeError: hipErrorPeerAccessUnsupported"}
     assert "e2e.node failed" in capsys.readouterr().err
+
+
+def test_rotation_copies_keep_small_read_sets_out_of_the_cache():
+    """Launch buffer sets (bench.rotation_copies): reads summed over the sets
+    reach the target, so a launch never finds its input in the 256 MB
+    Infinity Cache; batches that read >= the target keep one set."""
+    import bench
+    mib = 1 << 20
+    # headline: 64 x 32 MiB frames, Mean reads all 2 GiB
+    assert bench.rotation_copies(2048 * mib, "mean", False, 1024) == 1
+    assert bench.rotation_copies(2048 * mib, "decimate", False, 1024) == 1
+    # config V: one 512 MiB volume; Decimate reads every other row and plane
+    assert bench.rotation_copies(512 * mib, "mean", True, 1024) == 2
+    assert bench.rotation_copies(512 * mib, "decimate", True, 1024) == 8
+    # config C1b: 1024 x 512^2 u8 = 256 MiB, Decimate reads half the rows
+    assert bench.rotation_copies(256 * mib, "max", False, 1024) == 4
+    assert bench.rotation_copies(256 * mib, "decimate", False, 1024) == 8
+    # off, and the cap
+    assert bench.rotation_copies(512 * mib, "decimate", True, 0) == 1
+    assert bench.rotation_copies(mib, "mean", False, 1024) == 64
