@@ -2321,9 +2321,13 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             const char* v = std::getenv("AQZ_BAND_STAGING");
             return v && std::strcmp(v, "0") == 0;
         }();
-        // Aligned frames of 5-8 tiles per row band (the headline's 4096 u16
-        // pixels, 3072, 4096 f32) stage every level too, in 8-wave
-        // workgroups, so each level's band leaves as one contiguous span.
+        // Aligned frames of 4-8 tiles per row band (the headline's 4096 u16
+        // pixels, 3072, 4096 f32, config C2's 2048 u16) stage every level
+        // too, in workgroups of one wave per tile, so each level's band
+        // leaves as one contiguous span.  4-tile bands joined in round 5,
+        // timed with the data in HBM (rotating buffer sets): C2 Mean 123.0-
+        // 123.5 -> 118.1-118.4 us, Decimate 76.7-76.9 -> 72.1-72.4
+        // (profiles/r05/c2knobs/ab.log).
         // On most MI355X boxes tried, row-major level rows at a >= 4 KiB
         // pitch written 512 B per wave ran 15-20% below the same kernel with
         // tile-order stores; staged bands remove that (headline 535 -> 463
@@ -2347,7 +2351,7 @@ AQZ_SHARDED(launch_cascade)(int dtype,
         if (band_force) {
             stage_mask |= band_force & all_levels;
             wide_max = 8;
-        } else if (band_aligned && stage_mask == 0 && band_waves >= 5 && band_waves <= 8 &&
+        } else if (band_aligned && stage_mask == 0 && band_waves >= 4 && band_waves <= 8 &&
                    band_lds_bytes(sizeof(T), outs, n_out, all_levels) <= band_lds_cap()) {
             stage_mask = all_levels;
             wide_max = 8;
