@@ -2862,7 +2862,27 @@ AQZ_SHARDED(launch_volume)(int dtype,
 #define AQZ_VOL(NL, NTL, UPW)                                                          \
     hipLaunchKernelGGL((volume_kernel<T, M, NL, NTL, UPW>), dim3(grid), dim3(256), 0, \
                        stream, p)
+            // Decimate launches of 128 or more plane groups (two or more
+            // config-V volumes) take the plane groups fastest in the unit
+            // order, so the units in flight spread over many planes: four
+            // 1024^2 x 256 volumes 172.1-172.3 -> 148.1-149.0 us, data in HBM
+            // (profiles/r05/vzfast/ab.log); one volume (64 groups) loses
+            // 1-2% that way and keeps columns fastest.  Its reads never set
+            // the address bits of odd rows and odd planes.
+            // $AQZ_VOLUME_ZFAST=0 / 1: never / always (nontemporal loads).
+            static const int zf_env = int_env("AQZ_VOLUME_ZFAST", -1);
+            const bool zfast = zf_env >= 0 ? zf_env != 0 : (n_planes >> n_out) >= 128;
             if constexpr (M == kDecimate) {
+                if (upw == 2 && zfast && ntl) {
+                    constexpr int CZ = 16 / int(sizeof(T));
+                    if (n_out == 1)
+                        hipLaunchKernelGGL((volume_kernel<T, M, 1, true, 2, CZ, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                    else
+                        hipLaunchKernelGGL((volume_kernel<T, M, 2, true, 2, CZ, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                    return hipGetLastError();
+                }
                 if (upw == 2) {
                     if (n_out == 1 && ntl)
                         AQZ_VOL(1, true, 2);

@@ -179,6 +179,10 @@ BATCH_GEOMETRIES = {
     # units divide by 4: with column edges, and with one fused level (NL = 1)
     "3d_fused_oddw_even_h": ([(201, 64, 8), (101, 32, 4), (51, 16, 2)], 8, 2),
     "3d_fused_one_level": ([(256, 64, 4), (128, 32, 2)], 4, 2),
+    # 128 plane groups and more: Decimate takes the plane groups fastest in
+    # the unit order (round 5); column edges in the second
+    "3d_fused_many_groups": ([(64, 32, 8), (32, 16, 4), (16, 8, 2)], 512, 2),
+    "3d_fused_many_groups_edge": ([(72, 40, 8), (36, 20, 4), (18, 10, 2)], 520, 2),
     # level rows that split 64-B bursts: band-staged stores when a row band
     # is <= 4 tiles (1500 px u16), direct stores from band-aligned
     # workgroups for wider bands (2600 px u16 / f32, i64)
