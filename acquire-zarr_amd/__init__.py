@@ -53,7 +53,7 @@ EXPORTS = (
     "aqz_node_handle", "aqz_node_run_host_batch", "aqz_node_last_error",
     "aqz_node_add_frame", "aqz_node_take_frame", "aqz_node_flush",
     "aqz_node_run_device_batch", "aqz_node_wait_input", "aqz_ds_wait_input",
-    "aqz_node_set_level_tiling",
+    "aqz_node_set_level_tiling", "aqz_ds_input_pending", "aqz_node_inputs_released",
 )
 
 
@@ -220,6 +220,8 @@ def lib() -> ctypes.CDLL:
     L.aqz_node_wait_input.argtypes = [vp]
     L.aqz_node_set_level_tiling.argtypes = [vp, u32, u32, u32]
     L.aqz_ds_wait_input.argtypes = [vp]
+    L.aqz_ds_input_pending.argtypes = [vp, ctypes.POINTER(i32)]
+    L.aqz_node_inputs_released.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.aqz_node_run_device_batch.argtypes = [vp, vp, i32, u32, ctypes.POINTER(vp),
                                             ctypes.POINTER(u32), vp, u32]
     _lib = L
@@ -808,6 +810,13 @@ class Node:
         caller may reuse its buffers); their levels may still be running."""
         self._check(lib().aqz_node_wait_input(self._h))
         self._inflight.clear()
+
+    def inputs_released(self) -> int:
+        """aqz_node_inputs_released: how many of the frames added so far (a
+        prefix, in add order) no upload still reads — non-blocking."""
+        r = ctypes.c_uint64(0)
+        self._check(lib().aqz_node_inputs_released(self._h, ctypes.byref(r)))
+        return r.value
 
     def __del__(self):
         self.close()

@@ -131,12 +131,40 @@ wave_any(bool p)
     return __builtin_amdgcn_ballot_w64(p) != 0;
 }
 
+#ifdef AQZ_NAN_FIXUP_DIVERGENT
+// The round-5 lane-divergent form (branches on the NaN lanes only), kept for
+// the regression probe (tools/divergent/, tests/test_gpu_divergent.py).
+template<typename T>
+__device__ __forceinline__ T
+x86_add_branchy(T x, T y)
+{
+    using FB = float_bits<T>;
+    using U = typename FB::U;
+    const T s = x + y;
+    U r;
+    if (x != x)
+        r = __builtin_bit_cast(U, x) | FB::quiet();
+    else if (y != y)
+        r = __builtin_bit_cast(U, y) | FB::quiet();
+    else if (s != s)
+        r = FB::default_nan();
+    else
+        return s;
+    return __builtin_bit_cast(T, r);
+}
+#endif
+
 template<typename T>
 __device__ __forceinline__ T
 mean4(T a, T b, T c, T d)
 {
     if constexpr (std::is_floating_point_v<T>) {
         const T r = (((a + b) + c) + d) / T(4);
+#ifdef AQZ_NAN_FIXUP_DIVERGENT
+        if (__builtin_expect(r != r, 0))
+            return x86_add_branchy(x86_add_branchy(x86_add_branchy(a, b), c), d);
+        return r;
+#endif
         if (__builtin_expect(wave_any(r != r), 0)) {
             // the chain's first NaN is the value (x86 keeps it through the
             // later adds and the divide); other lanes keep theirs
@@ -159,6 +187,11 @@ mean2(T a, T b)
 {
     if constexpr (std::is_floating_point_v<T>) {
         const T r = (a + b) / T(2);
+#ifdef AQZ_NAN_FIXUP_DIVERGENT
+        if (__builtin_expect(r != r, 0))
+            return x86_add_branchy(a, b);
+        return r;
+#endif
         if (__builtin_expect(wave_any(r != r), 0)) {
             const T n = x86_add(a, b);
             return (r != r) ? n : r;
@@ -2387,7 +2420,10 @@ AQZ_SHARDED(launch_cascade)(int dtype,
             band_waves = 8;
             wide_max = 8;
         } else if (misaligned && band_waves > mis_max && (sizeof(T) == 2 || sizeof(T) == 4) &&
-                   (cols == CW || tile16) &&
+                   // exactly the tiles the dispatch below builds a rowwise
+                   // (RW) band kernel for (2-byte narrow tiles
+                   // have none)
+                   (cols == CW || (sizeof(T) == 4 && cols == CN)) &&
                    (mis_seg_env > 0 || (mis_seg_env < 0 && band_waves > 8))) {
             // Misaligned bands of more than 8 tiles (2- and 4-byte types, wide
             // tiles): balanced segments of at most 4 tiles

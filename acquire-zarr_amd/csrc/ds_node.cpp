@@ -71,6 +71,7 @@ struct PeerStage
     uint8_t* stage = nullptr; // 2 slots of slot_bytes
     size_t slot_bytes = 0;
     uint32_t next_slot = 0;
+    std::vector<int> peers_on; // source ordinals this device has peer access to
 };
 
 } // namespace
@@ -95,6 +96,7 @@ struct aqz_node
     struct Add
     {
         uint32_t handle = 0;
+        uint64_t frame = 0; // the stream's frame index (aqz_node_inputs_released)
         bool settled = false;
         std::vector<aqz_level_take> takes;
         std::vector<std::vector<uint8_t>> bufs;
@@ -224,16 +226,20 @@ peer_stage(aqz_node* n, uint32_t h, int src_device, size_t slot)
                     return hip_fail(n, e, "node device batch: event");
         if ((e = hipEventCreateWithFlags(&p.done, hipEventDisableTiming)) != hipSuccess)
             return hip_fail(n, e, "node device batch: event");
-        // direct xGMI access to the batch's GPU where the pair has it (the
-        // copies work either way; this keeps them off any host bounce)
+    }
+    // direct xGMI access to the batch's GPU where the pair has it (the copies
+    // work either way; this keeps them off any host bounce), for every source
+    // ordinal a call names, not only the first one
+    if (dev != src_device &&
+        std::find(p.peers_on.begin(), p.peers_on.end(), src_device) == p.peers_on.end()) {
         int can = 0;
-        if (dev != src_device && hipDeviceCanAccessPeer(&can, dev, src_device) == hipSuccess &&
-            can) {
+        if (hipDeviceCanAccessPeer(&can, dev, src_device) == hipSuccess && can) {
             e = hipDeviceEnablePeerAccess(src_device, 0);
             if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
                 return hip_fail(n, e, "node device batch: peer access");
             (void)hipGetLastError(); // clear "already enabled"
         }
+        p.peers_on.push_back(src_device);
     }
     if (p.slot_bytes < slot) {
         for (hipStream_t s : { p.pull, p.run, p.push })
@@ -486,6 +492,7 @@ aqz_node_add_frame(aqz_node* n, const void* host_frame, size_t nbytes)
         n->adds.emplace_back();
         aqz_node::Add& a = n->adds.back();
         a.handle = h;
+        a.frame = n->frames;
         a.takes.assign(nl, aqz_level_take{});
         a.bufs.resize(nl);
         for (uint32_t L = 1; L < nl; ++L) {
@@ -906,6 +913,33 @@ aqz_node_run_device_batch(aqz_node* n,
                 out_counts[L] = units * n->per_unit[L];
         }
         n->frames += n_frames;
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(n);
+    }
+}
+
+int
+aqz_node_inputs_released(aqz_node* n, uint64_t* released)
+{
+    try {
+        if (!n || !released)
+            return AQZ_INVALID_ARGUMENT;
+        // adds are in submission order; only a handle's add in flight can
+        // still read its frame, and the earliest such one bounds the prefix
+        uint64_t r = n->frames;
+        for (const auto& a : n->adds) {
+            if (a.settled || n->in_flight[a.handle] != &a)
+                continue;
+            int pending = 0;
+            if (int rc = aqz_ds_input_pending(n->ds[a.handle], &pending))
+                return fail(n, rc, "node_inputs_released: handle " + std::to_string(a.handle));
+            if (pending) {
+                r = a.frame;
+                break;
+            }
+        }
+        *released = r;
         return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(n);

@@ -672,12 +672,21 @@ add_host_frame(aqz_ds* ds, const void* host_frame)
     HIP_TRY(ds,
             hipMemcpyAsync(ds->d_in, src, nbytes, hipMemcpyHostToDevice, ds->stream),
             "hipMemcpyAsync H2D");
-    HIP_TRY(ds, hipEventRecord(ds->h2d_done, ds->stream), "hipEventRecord");
+    // From here on the copy may still read the caller's frame: every way out
+    // waits for it first, so that a failed add, too, releases the frame only
+    // once nothing reads it (aqz_ds_wait_input's contract).
+    if (const hipError_t e = hipEventRecord(ds->h2d_done, ds->stream); e != hipSuccess) {
+        (void)hipStreamSynchronize(ds->stream);
+        return ds->fail(e, "hipEventRecord");
+    }
     int rc = process_input(ds, ds->d_in);
-    if (rc)
+    if (rc == AQZ_OK)
+        rc = eager_readback(ds);
+    if (rc != AQZ_OK) {
+        if (!ds->staged)
+            (void)hipEventSynchronize(ds->h2d_done);
         return rc;
-    if ((rc = eager_readback(ds)) != AQZ_OK)
-        return rc;
+    }
     if (!ds->staged) {
         // the caller may reuse its frame as soon as we return
         HIP_TRY(ds, hipEventSynchronize(ds->h2d_done), "hipEventSynchronize");
@@ -1361,6 +1370,24 @@ aqz_ds_wait_input(aqz_ds* ds)
             return AQZ_OK;
         std::unique_lock<std::mutex> lk(a.m);
         a.cv.wait(lk, [&] { return a.input == nullptr; });
+        return AQZ_OK;
+    } catch (...) {
+        return ABI_GUARD_FAIL(ds);
+    }
+}
+
+int
+aqz_ds_input_pending(aqz_ds* ds, int* pending)
+{
+    try {
+        if (!ds || !pending)
+            return AQZ_INVALID_ARGUMENT;
+        *pending = 0;
+        auto& a = ds->async;
+        if (a.worker.joinable()) {
+            std::lock_guard<std::mutex> lk(a.m);
+            *pending = a.input != nullptr;
+        }
         return AQZ_OK;
     } catch (...) {
         return ABI_GUARD_FAIL(ds);

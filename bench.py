@@ -21,6 +21,7 @@ through the streaming API, the path's real end-to-end rate).
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -761,7 +762,8 @@ def main():
                     e2e["node_device_batch"] = aux_leg(
                         "e2e.node_device_batch", measure_node_device_batch, aqz, torch, geo,
                         dtype, method, d_in, outs, counts, B, frame_bytes, device,
-                        [r % n_vis for r in range(world)], stream, avg_launch_s)
+                        [r % n_vis for r in range(world)], stream, avg_launch_s,
+                        local_launch_shared=rehearsal)
                 if rehearsal:
                     e2e["node"]["rehearsal"] = f"{world} handles on {n_vis} device(s)"
             else:
@@ -1315,109 +1317,55 @@ def measure_e2e(aqz, geo, dtype, method, n_frames, device, tile=None):
         res["tiled_take_ms_per_frame"] = round(el / n_frames * 1e3, 3)
         res["tile"] = list(tile)
         res["tiled_one_pass_runs"] = ds.stream_tiled_runs()
-        res["async_overlap"] = measure_async_overlap(ds, geo, frames, n_frames, tile)
-        res["async_overlap_ms_per_frame"] = res["async_overlap"]["async_overlap_ms_per_frame"]
-        res["async_take_ms_per_frame"] = res["async_overlap"]["async_take_ms_per_frame"]
+        if (W, H, np.dtype(dtype), tuple(tile)) == (4096, 4096, np.dtype(np.uint16), (256, 256)):
+            ds.close()  # the probe's handle takes its place on this GPU
+            res["async_overlap"] = aux_leg("e2e.async_overlap", measure_async_overlap, device)
+            return res
     ds.close()
     return res
 
 
-class HostTiler:
-    """Level 0 chunked on the host the way the patched
-    MultiscaleArray::write_frame has arrays_[0] do it while the GPU works
-    (Array::write_frame_to_chunks_, array.cpp:507-622: tile rows copied into
-    chunk-tile order, OpenMP over tiles): numpy copies of tile-row bands on
-    `threads` host threads (numpy releases the GIL inside the copy)."""
-
-    def __init__(self, H, W, dtype, tile, threads=16):
-        import concurrent.futures as cf
-        self.H, self.W = H, W
-        self.tr, self.tc = tile
-        self.nty, self.ntx = -(-H // self.tr), -(-W // self.tc)
-        self.buf = np.zeros((self.nty, self.ntx, self.tr, self.tc), dtype)
-        self.pool = cf.ThreadPoolExecutor(max_workers=threads)
-
-    def _band(self, frame, ty):
-        r0 = ty * self.tr
-        rows = min(self.tr, self.H - r0)
-        for tx in range(self.ntx):
-            c0 = tx * self.tc
-            cols = min(self.tc, self.W - c0)
-            self.buf[ty, tx, :rows, :cols] = frame[r0:r0 + rows, c0:c0 + cols]
-
-    def __call__(self, frame):
-        list(self.pool.map(lambda ty: self._band(frame, ty), range(self.nty)))
-        return self.buf
-
-    def close(self):
-        self.pool.shutdown()
-
-
-def measure_async_overlap(ds, geo, frames, n_frames, tile):
+def measure_async_overlap(device, frames=24):
     """SURVEY §8(f) row 1 as the patched MultiscaleArray::write_frame runs it
-    (acquire-zarr-hip.patch; multiscale.array.cpp:57-74,291-325): per frame,
-    add_frame_async (upload + pyramid + level tiling queued on the GPU), level
-    0 chunked on the host meanwhile, wait, then take_frame_tiled of every
-    level.  Beside it the same work in sequence (add_frame, then the host
-    tiling, then the takes) and the host tiling alone.  Every tile the takes
-    return for the last frame is compared bit for bit with the same frame
-    taken through the synchronous calls."""
-    W, H, _ = geo[0]
-    tiler = HostTiler(H, W, frames[0].dtype, tile)
-    n_lv = len(geo)
-
-    def takes():
-        return [ds.take_frame_tiled(L, tile[0], tile[1]) for L in range(1, n_lv)]
-
-    for i in range(3):  # warm
-        ds.add_frame_async(frames[i % 4])
-        tiler(frames[i % 4])
-        ds.wait()
-        takes()
-    t0 = time.perf_counter()
-    for i in range(n_frames):
-        ds.add_frame_async(frames[i % 4])
-        tiler(frames[i % 4])
-        ds.wait()
-        last_async = takes()
-    overlap = (time.perf_counter() - t0) / n_frames
-    # the takes in the background job too (aqz_ds_add_frame_async_take):
-    # the levels' D2H overlaps the host tiling as the upload does
-    tl = [None] + [tuple(tile)] * (n_lv - 1)
-    for i in range(3):
-        ds.add_frame_async_take(frames[i % 4], tl)
-        tiler(frames[i % 4])
-        ds.wait_takes()
-    t0 = time.perf_counter()
-    for i in range(n_frames):
-        ds.add_frame_async_take(frames[i % 4], tl)
-        tiler(frames[i % 4])
-        last_take = ds.wait_takes()[1:]
-    overlap_take = (time.perf_counter() - t0) / n_frames
-    t0 = time.perf_counter()
-    for i in range(n_frames):
-        ds.add_frame(frames[i % 4])
-        tiler(frames[i % 4])
-        last_sync = takes()
-    seq = (time.perf_counter() - t0) / n_frames
-    t0 = time.perf_counter()
-    for i in range(n_frames):
-        tiler(frames[i % 4])
-    host = (time.perf_counter() - t0) / n_frames
-    tiler.close()
-    # both loops end on frames[(n_frames - 1) % 4]
-    same = all(a is not None and b is not None and c is not None and
-               np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and
-               np.array_equal(c[0].reshape(-1), b[0].reshape(-1)) and np.array_equal(c[1], b[1])
-               for a, b, c in zip(last_async, last_sync, last_take))
-    return {"async_overlap_ms_per_frame": round(overlap * 1e3, 3),
-            "async_take_ms_per_frame": round(overlap_take * 1e3, 3),
-            "sequential_ms_per_frame": round(seq * 1e3, 3),
-            "host_l0_tiling_ms_per_frame": round(host * 1e3, 3),
-            "host_threads": 16,
-            "async_equals_sync": bool(same),
-            "path": "add_frame_async; level 0 tiled on host threads; wait; "
-                    "take_frame_tiled(every level)"}
+    (acquire-zarr-hip.patch; multiscale.array.cpp:57-74,291-325), timed by the
+    C++ caller tools/write_frame_probe.cpp (the reference's
+    Array::write_frame_to_chunks_ restated: level 0 chunked by an OpenMP loop
+    of row copies with the zero scan, array.cpp:507-622, chunk.cpp:17-58),
+    run as a child process on this GPU: per 4096^2 u16 frame, 5 levels, 256^2
+    chunks.  `sync` is the reference's order (host-tile level 0, add_frame,
+    take every level); `async` starts the add first and tiles level 0 while
+    the frame crosses PCIe; `async_take` also runs the level takes in the
+    add's background job.  The parts alone: host_tile, h2d_pageable (upload
+    of a pageable frame) and gpu_side (everything but the host tiling); the
+    ideal overlap is the larger of host_tile and gpu_side.  Bit-exactness of
+    these call orders is the GPU tests' (tests/test_gpu_adapter.py overlap /
+    double / asyncsync modes), not this timing's."""
+    import subprocess
+    probe = os.path.join(ROOT, "tools", "write_frame_probe")
+    if not os.path.exists(probe):
+        return {"skipped": "tools/write_frame_probe not built (make -C acquire-zarr_amd probe)"}
+    env = dict(os.environ, AQZ_GPU_DEVICE=str(device))
+    r = subprocess.run([probe, str(frames), "2"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    if r.returncode != 0:
+        return {"error": f"write_frame_probe exit {r.returncode}: {r.stderr.strip()[-300:]}"}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    ms = d["ms_per_frame"]
+    ideal = max(ms["host_tile"], ms["gpu_side"])
+    return {"sequential_ms_per_frame": ms["sync"],
+            "async_overlap_ms_per_frame": ms["async"],
+            "async_take_ms_per_frame": ms["async_take"],
+            "host_l0_tiling_ms_per_frame": ms["host_tile"],
+            "h2d_pageable_ms_per_frame": ms["h2d_pageable"],
+            "gpu_side_ms_per_frame": ms["gpu_side"],
+            "ideal_overlap_ms_per_frame": ideal,
+            "async_over_ideal": round(ms["async"] / ideal, 3),
+            "async_take_over_ideal": round(ms["async_take"] / ideal, 3),
+            "async_phases_ms": d["async_phases_ms"],
+            "gpu_tiled_ms_per_frame": ms["gpu_tiled"],
+            "omp_threads": d["omp_threads"], "frames": frames,
+            "path": "tools/write_frame_probe (C++ caller, OpenMP level-0 chunking): "
+                    "add_frame_async; level 0 chunked on the host; wait; tiled takes"}
 
 
 def _fs_type(path):
@@ -1547,7 +1495,8 @@ def aux_leg(name, fn, *args, **kwargs):
 
 
 def measure_node_device_batch(aqz, torch, geo, dtype, method, d_in, outs, counts, B,
-                              frame_bytes, device, devices, stream, local_launch_s, reps=5):
+                              frame_bytes, device, devices, stream, local_launch_s, reps=5,
+                              local_launch_shared=False):
     """BASELINE config F's multi-GPU form through the library
     (aqz_node_run_device_batch): len(devices) copies of this
     rank's device-resident batch, on this GPU, dealt over `devices` in whole
@@ -1590,11 +1539,15 @@ def measure_node_device_batch(aqz, torch, geo, dtype, method, d_in, outs, counts
     finally:
         node.close()
     W, H, _ = geo[0]
-    one_gpu_ms = ND * local_launch_s * 1e3
+    # the one-GPU reference time is this rank's own launch time from the
+    # main region; where handles (or ranks) share a device that time was
+    # itself slowed by the sharing, so no speed-up is reported
+    shared = len(set(devices)) < len(devices) or local_launch_shared
+    one_gpu_ms = None if shared else ND * local_launch_s * 1e3
     out = {"value": round(ND * B * W * H / (ms * 1e-3) / 1e9, 3), "unit": "GPixels/s",
            "ms_per_call": round(ms, 4), "frames_per_call": ND * B, "devices": list(devices),
-           "one_gpu_ms_same_frames": round(one_gpu_ms, 4),
-           "speedup_vs_one_gpu": round(one_gpu_ms / ms, 3),
+           "one_gpu_ms_same_frames": None if one_gpu_ms is None else round(one_gpu_ms, 4),
+           "speedup_vs_one_gpu": None if one_gpu_ms is None else round(one_gpu_ms / ms, 3),
            "check": ("bit-exact" if exact else "MISMATCH") +
                     f" (all {ND} blocks vs this rank's own batch)",
            "path": "aqz_node_run_device_batch: this GPU's batch dealt in whole shard units, "
@@ -1654,15 +1607,25 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
         sbest = el if sbest is None else min(sbest, el)
 
     # the drop-in's node mode (integration/src/streaming/downsampler.hip.cpp
-    # with $AQZ_GPU_DEVICES), the consumer side: per frame add, wait until it
-    # is uploaded (aqz_node_wait_input: the frame queue may then reuse the
-    # buffer) and take every ready level; a flush and a last drain at the end
+    # with $AQZ_GPU_DEVICES), the consumer side as Downsampler::release_frame
+    # runs it: per frame add, no wait — the adapter keeps the frame's buffer
+    # while its upload may run and hands the frame queue a spare, recycling
+    # the kept buffers as aqz_node_inputs_released passes them — and take
+    # every ready level; a flush and a last drain at the end
     # (MultiscaleArray::close_).  The queue's copy into its slot happens on
-    # the producer thread and is not timed.
+    # the producer thread and is not timed.  The buffers here are the frame
+    # list's own (nothing rewrites them), so the bookkeeping is kept without
+    # the spare allocations.
     def dropin():
-        for f in frames:
+        kept = collections.deque()
+        spares = 0
+        for k, f in enumerate(frames):
             node.add_frame(f)
-            node.wait_input()
+            released = node.inputs_released()
+            while kept and kept[0][0] < released:
+                kept.popleft()
+                spares += 1
+            kept.append((k, f))
             for L in levels:
                 while node.take_frame(L) is not None:
                     pass
@@ -1670,6 +1633,7 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
         for L in levels:
             while node.take_frame(L) is not None:
                 pass
+        return spares
     dropin()  # warm
     dbest = None
     for _ in range(3):
@@ -1686,9 +1650,10 @@ def measure_e2e_node(aqz, torch, geo, dtype, method, d_in, n, devices):
             "devices": list(devices), "shard_unit": node.unit,
             "stream_ms_per_frame": round(sbest / len(frames) * 1e3, 3),
             "dropin_ms_per_frame": round(dbest / len(frames) * 1e3, 3),
-            "dropin_path": "per pageable frame: aqz_node_add_frame, aqz_node_wait_input, every "
-                           "ready level taken; flush at the end (the drop-in's "
-                           "$AQZ_GPU_DEVICES mode, consumer side)",
+            "dropin_path": "per pageable frame: aqz_node_add_frame, no upload wait (the "
+                           "adapter keeps the buffer, recycled by aqz_node_inputs_released), "
+                           "every ready level taken; flush at the end (the drop-in's "
+                           "$AQZ_GPU_DEVICES mode, consumer side, Downsampler::release_frame)",
             "stream_path": f"aqz_node_add_frame of {len(frames)} pageable frames, every level "
                            "taken when ready, then aqz_node_flush",
             "path": f"aqz_node_run_host_batch over handles on devices {list(devices)}, "

@@ -204,6 +204,14 @@ int aqz_ds_poll(aqz_ds* ds, int* done);
 int aqz_ds_wait_input(aqz_ds* ds);
 
 /*
+ * Non-blocking aqz_ds_wait_input: *pending = 1 while the pending
+ * aqz_ds_add_frame_async[_take] job may still read its host frame, 0 once the
+ * caller may reuse it (or nothing is pending).  Clears no status.  No
+ * reference counterpart; aqz_node_inputs_released is built on it.
+ */
+int aqz_ds_input_pending(aqz_ds* ds, int* pending);
+
+/*
  * One level's part in aqz_ds_add_frame_async_take.
  *   mode AQZ_TAKE_NONE: nothing (the level is taken later, or not at all);
  *   AQZ_TAKE_INTO: right behind the add, take the level's frame if it has
@@ -732,6 +740,19 @@ int aqz_node_flush(aqz_node* node);
  * the single-handle adapter waits for the whole add.
  */
 int aqz_node_wait_input(aqz_node* node);
+
+/*
+ * Non-blocking: *released = the number of frames, counted from the node's
+ * first aqz_node_add_frame, that no add in flight still reads — every frame
+ * before the earliest one whose upload may still run (all of them when none
+ * is).  A caller that owns the frames' buffers recycles each one whose index
+ * is below *released; the drop-in's node mode keeps the consumer's frame
+ * buffers this way instead of waiting for every upload
+ * (integration/src/streaming/downsampler.hip.cpp, Downsampler::release_frame;
+ * the buffers are the frame queue's, which FrameQueue::pop hands over by swap,
+ * frame.queue.cpp:48-74).
+ */
+int aqz_node_inputs_released(aqz_node* node, uint64_t* released);
 
 /* Last error message of the node (never NULL; "" when none). */
 const char* aqz_node_last_error(const aqz_node* node);

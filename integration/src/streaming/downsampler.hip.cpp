@@ -11,6 +11,8 @@
 //   take_frame(level, out)       downsampler.cpp:403-414  -> aqz_ds_take_frame
 //   add_frame_async(frame)       new -> aqz_ds_add_frame_async_take
 //   wait()                       new                      -> aqz_ds_wait
+//   release_frame(frame)         new                      -> wait(), or (node mode)
+//                                                            keeps the buffer
 //   take_frame_tiled(level, t)   new -> aqz_ds_take_frame_tiled
 //   level_is_tiled(level)        new
 //   flush()                      new                      -> (node mode) aqz_node_flush
@@ -25,8 +27,16 @@
 // several frames' pyramids and level copies run at once, each GPU over its
 // own PCIe link.  add_frame_async hands the frame to the next GPU and wait()
 // returns once it is uploaded (aqz_node_wait_input), not when its levels are
-// done; take_frame / take_frame_tiled hand out, in emission order, the next
-// level frame that is ready.  The patched MultiscaleArray takes every ready
+// done.  release_frame() — what the patched MultiscaleArray calls once level
+// 0 is written — does not wait at all: it keeps the frame's buffer while the
+// GPU may still read it and swaps a spare of the same size into the caller's
+// vector (the frame queue's, which FrameQueue::pop fills by swap and push
+// refills by resize + memcpy, frame.queue.cpp:20-74, and which
+// process_frame_queue_ never reads after write_frame, zarr.stream.cpp:
+// 1671-1685).  So uploads to different GPUs overlap, and the buffers recycle
+// as aqz_node_inputs_released reports their uploads done: at most one per
+// GPU plus one spare, no copy.  take_frame / take_frame_tiled hand out, in
+// emission order, the next level frame that is ready.  The patched MultiscaleArray takes every ready
 // frame per level after each add and calls flush() before it closes its
 // arrays, so each level receives exactly the frames, in the order, that the
 // reference's add_frame + take_frame loop produces (multiscale.array.cpp:
@@ -203,8 +213,10 @@ zarr::Downsampler::Downsampler(std::shared_ptr<ArrayConfig> config,
 
 zarr::Downsampler::~Downsampler()
 {
-    aqz_node_destroy(node_); // each handle settles its add in flight first
-    aqz_ds_destroy(gpu_);    // settles a pending add_frame_async first
+    // each handle settles its add in flight first, so no upload still reads
+    // a buffer in node_inputs_ when the members go
+    aqz_node_destroy(node_);
+    aqz_ds_destroy(gpu_); // settles a pending add_frame_async first
 }
 
 void
@@ -239,8 +251,13 @@ zarr::Downsampler::add_frame_async(std::vector<uint8_t>& frame)
     if (node_) {
         // the previous frame may still be uploading to its GPU; this one
         // goes to the next GPU in the deal
+        if (node_caller_frame_) {
+            wait(); // an earlier add_frame_async nobody released
+        }
         const int rc = aqz_node_add_frame(node_, frame.data(), frame.size());
         EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+        node_caller_frame_ = frame.data();
+        ++node_added_;
         pending_ = true;
         return;
     }
@@ -289,8 +306,13 @@ void
 zarr::Downsampler::wait()
 {
     if (node_) {
-        // every frame handed over so far is uploaded: the caller may reuse it
+        // the caller's frame of the last add is uploaded: the caller may
+        // reuse it (buffers release_frame kept need no wait)
         pending_ = false;
+        if (!node_caller_frame_) {
+            return;
+        }
+        node_caller_frame_ = nullptr;
         const int rc = aqz_node_wait_input(node_);
         EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
         return;
@@ -307,6 +329,39 @@ zarr::Downsampler::wait()
             holding_[level] = 1;
         }
     }
+}
+
+void
+zarr::Downsampler::release_frame(std::vector<uint8_t>& frame)
+{
+    if (!node_ || !node_caller_frame_ || frame.data() != node_caller_frame_ ||
+        frame.empty()) {
+        wait(); // one GPU: the add's takes are settled here, as before
+        return;
+    }
+    // Buffers whose uploads are done become spares (in stream order: the
+    // node reports a prefix of its frames).
+    uint64_t released = 0;
+    const int rc = aqz_node_inputs_released(node_, &released);
+    EXPECT(rc == AQZ_OK, "GPU downsampler: ", aqz_node_last_error(node_));
+    while (!node_inputs_.empty() && node_inputs_.front().first < released) {
+        node_spares_.push_back(std::move(node_inputs_.front().second));
+        node_inputs_.pop_front();
+    }
+    // Keep the caller's buffer (a vector swap moves no bytes: the node goes
+    // on reading the same memory) and give the caller a spare of its size.
+    ByteVector spare;
+    if (!node_spares_.empty()) {
+        spare = std::move(node_spares_.back());
+        node_spares_.pop_back();
+    }
+    ByteVector kept;
+    kept.swap(frame);
+    spare.resize(kept.size());
+    frame.swap(spare);
+    node_inputs_.emplace_back(node_added_ - 1, std::move(kept));
+    node_caller_frame_ = nullptr;
+    pending_ = false;
 }
 
 bool

@@ -25,10 +25,13 @@
 //     asyncsync as double, the second add synchronous (add_frame settles the
 //               pending add first: ADVICE r4)
 //     node      the patched MultiscaleArray with $AQZ_GPU_DEVICES naming
-//               several GPUs: add_frame_async, wait, then every READY frame
-//               per level (write_level_frames_); flush() and a last drain
-//               at the end (close_).  Only taken frames are written, `frame`
-//               = the add after which each came out; pattern must be "all"
+//               several GPUs: add_frame_async, release_frame (the adapter
+//               keeps the frame's buffer for the upload and hands back a
+//               spare, which the next frame is written into), then every
+//               READY frame per level (write_level_frames_); flush() and a
+//               last drain at the end (close_).  Only taken frames are
+//               written, `frame` = the add after which each came out;
+//               pattern must be "all"
 //   pattern: all | every3 (takes only after frames 2, 5, 8, ...)
 //   out.bin: per take, int64 {frame, level, has_frame, tiled, nbytes} then
 //            the bytes.
@@ -94,6 +97,7 @@ main(int argc, char** argv)
         // frames the way the frame queue hands them over: a vector per frame,
         // kept alive until the call that settles it (multiscale.array.cpp:57-74)
         std::vector<uint8_t> frame, frame2;
+        size_t released = 0, kept = 0; // node mode: buffers the adapter kept
 
         auto takes = [&](int k, bool tiled_takes) {
             if (!(pattern == "all" || (pattern == "every3" && k % 3 == 2)))
@@ -135,7 +139,14 @@ main(int argc, char** argv)
                 takes(k, mode == "overlap");
             } else if (mode == "node") {
                 ds.add_frame_async(frame);
-                ds.wait();
+                const uint8_t* handed = frame.data();
+                ds.release_frame(frame);
+                if (frame.size() != frame_bytes) {
+                    std::fprintf(stderr, "release_frame: spare of %zu bytes\n", frame.size());
+                    return 4;
+                }
+                ++released;
+                kept += frame.data() != handed;
                 drain(k);
             } else if (mode == "asyncsync") {
                 // frame k async; if the pattern takes nothing after it, frame
@@ -168,6 +179,8 @@ main(int argc, char** argv)
         if (mode == "node") {
             ds.flush(); // MultiscaleArray::close_
             drain(n_frames);
+            std::fprintf(stderr, "node: %zu of %zu frames' buffers kept by the adapter\n", kept,
+                         released);
         }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "adapter threw: %s\n", e.what());

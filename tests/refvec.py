@@ -63,7 +63,20 @@ GEOMETRIES = {
     # Z halves while XY is copied
     "zonly_16_6x6": ([(TIME, 0, 1, 1), (SPACE, 16, 2, 1), (SPACE, 6, 8, 1), (SPACE, 6, 8, 1)],
                      16, "all"),
+    # BASELINE config C1a, the reference's own example
+    # (examples/stream-raw-multiscale-to-filesystem.c:13-67,80-90): 5-D
+    # t10/5/2 c8/4/2 z6/2/1 y48/16/1 x64/16/2, frames i*1000+j (u16 wraps),
+    # the 10 frames the example appends ...
+    "example_5d": ([(TIME, 10, 5, 2), (CHANNEL, 8, 4, 2), (SPACE, 6, 2, 1), (SPACE, 48, 16, 1),
+                    (SPACE, 64, 16, 2)], 10, "all"),
+    # ... and one whole timepoint of that array (8 channels x 6 planes), so
+    # every channel's Z pairs and the channel boundaries are pinned too
+    "example_5d_t0": ([(TIME, 10, 5, 2), (CHANNEL, 8, 4, 2), (SPACE, 6, 2, 1), (SPACE, 48, 16, 1),
+                       (SPACE, 64, 16, 2)], 48, "all"),
 }
+
+# geometries whose frames are the example's pattern, not seeded noise
+EXAMPLE_GEOMETRIES = ("example_5d", "example_5d_t0")
 
 
 def case_name(geom, dtype, method):
@@ -82,6 +95,12 @@ def make_inputs(geom, dtype, seed):
     dims, n_frames, _ = GEOMETRIES[geom]
     h, w = dims[-2][1], dims[-1][1]
     dt = np.dtype(dtype)
+    if geom in EXAMPLE_GEOMETRIES:
+        # the example's `frame[j] = i * 1000 + j` into a uint16_t (mod 2^16),
+        # the same numbers in every dtype
+        i = np.arange(n_frames, dtype=np.int64)[:, None]
+        j = np.arange(h * w, dtype=np.int64)[None, :]
+        return ((i * 1000 + j) & 0xFFFF).astype(dt).reshape(n_frames, h, w)
     rng = np.random.default_rng(seed)
     shape = (n_frames, h, w)
     if dt.kind == "f":

@@ -300,3 +300,56 @@ def test_poll_reports_the_async_job(aqz):
         assert ds.take_frame(1) is not None
     finally:
         ds.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["x2", "x3"])
+def test_node_inputs_released_lets_buffers_recycle(aqz, oracle, devices):
+    """The drop-in's node mode without upload waits (Downsampler::
+    release_frame): a frame buffer goes back to the producer as soon as
+    aqz_node_inputs_released passes its index, and is overwritten with a
+    later frame while other frames are still in flight.  The count is a
+    prefix that never decreases and reaches every frame after the flush, and
+    the levels are still exactly one oracle stream's."""
+    import collections
+    dims = STREAM_CASES["vol_z16"][0]
+    geo = aqz.level_geometry(aqz.plan_levels(dims))
+    w, h, _ = geo[0]
+    n = 40
+    frames = random_frames(np.random.default_rng(17), np.uint16, (n, h, w))
+    node = aqz.Node(geo, np.uint16, aqz.MEAN, devices)
+    got = {L: [] for L in range(1, len(geo))}
+    kept = collections.deque()  # (frame index, buffer) the node may read
+    spares = []
+    allocated = 0
+    last = 0
+    try:
+        for k in range(n):
+            buf = spares.pop() if spares else None
+            if buf is None:
+                buf = np.empty((h, w), np.uint16)
+                allocated += 1
+            np.copyto(buf, frames[k])   # the producer's copy into a free slot
+            node.add_frame(buf)
+            released = node.inputs_released()
+            assert last <= released <= k + 1
+            last = released
+            while kept and kept[0][0] < released:
+                spares.append(kept.popleft()[1])
+            kept.append((k, buf))
+            for L in got:
+                while (r := node.take_frame(L)) is not None:
+                    got[L].append(r)
+        node.flush()
+        assert node.inputs_released() == n
+        for L in got:
+            while (r := node.take_frame(L)) is not None:
+                got[L].append(r)
+    finally:
+        node.close()
+    # at most one buffer in flight per handle, plus the one being filled
+    assert allocated <= len(devices) + 2, allocated
+    want = _oracle_levels(oracle, geo, np.uint16, aqz.MEAN, frames)
+    for L in got:
+        assert len(got[L]) == len(want[L])
+        for k, (a, b) in enumerate(zip(got[L], want[L])):
+            assert_parity(a, b, f"recycled L{L} frame {k}")

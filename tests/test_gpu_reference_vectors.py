@@ -3,8 +3,11 @@
 zarr::Downsampler compiled unmodified, tests/golden/make_reference_vectors.py).
 
 * the streaming drop-in (aqz_ds_add_frame / aqz_ds_take_frame) replays all
-  320 cases — 8 geometries x 10 dtypes x 4 methods — frame by frame, with the
-  reference's frame readiness, untaken frames and odd-Z pass-through;
+  400 cases — 10 geometries x 10 dtypes x 4 methods — frame by frame, with the
+  reference's frame readiness, untaken frames and odd-Z pass-through; two of
+  the geometries are BASELINE config C1a itself (the reference example's 5-D
+  t10 c8 z6 y48 x64 array and its frames i*1000+j: the 10 frames the example
+  appends, and one whole timepoint);
 * the device batch (aqz_ds_run_device_batch, the bench path) reproduces each
   level's frames of every geometry whose levels are all taken after every
   frame.

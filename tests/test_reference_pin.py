@@ -5,9 +5,11 @@ oracle/_ref — VERDICT r3 item 1).
 Committed fixtures (tests/golden/reference_vectors.{npz,json},
 reference_digests.json, made by tests/golden/make_reference_vectors.py from
 the reference) are checked wherever the suite runs:
-* the oracle reproduces every vector byte for byte — 8 geometries x 10 dtypes
+* the oracle reproduces every vector byte for byte — 10 geometries x 10 dtypes
   x 4 methods, with odd XY, odd Z pass-through, channels outside Z, copy
-  levels, untaken frames, NaN/inf/-0/subnormals and integer extremes;
+  levels, untaken frames, NaN/inf/-0/subnormals and integer extremes, and
+  BASELINE config C1a itself (the reference example's 5-D array and frames,
+  examples/stream-raw-multiscale-to-filesystem.c:13-67,80-90);
 * both planners (oracle and product) equal the reference's
   writer_configurations() level by level, scales included;
 * the product's method strings and metadata JSON equal the reference's
@@ -47,8 +49,8 @@ def _oracle_make(oracle):
 
 
 def test_fixture_covers_the_matrix():
-    assert len(MAN["geometries"]) == 8 and len(MAN["dtypes"]) == 10
-    assert len(CASES) == 320
+    assert len(MAN["geometries"]) == 10 and len(MAN["dtypes"]) == 10
+    assert len(CASES) == 400
     assert "3.1.1" in MAN["nlohmann_json"]
     # every case made at least one frame at every level, and some cases
     # have levels left untaken (has_frame False) on purpose
@@ -58,6 +60,24 @@ def test_fixture_covers_the_matrix():
         assert ev[:, 2].any()
         n_missing += int((ev[:, 2] == 0).sum())
     assert n_missing > 0
+
+
+def test_fixture_holds_config_c1a():
+    """BASELINE config C1a is the reference's own example: 5-D t10 c8 z6 y48
+    x64 u16, frames i*1000+j, the zero-initialised method (Decimate) — its
+    levels and pixels as the reference made them."""
+    g = MAN["geometries"]["example_5d"]
+    assert [tuple(d) for d in g["dims"]] == [(2, 10, 5, 2), (1, 8, 4, 2), (0, 6, 2, 1),
+                                             (0, 48, 16, 1), (0, 64, 16, 2)]
+    assert g["frames"] == 10 and g["geometry"] == [[64, 48, 6], [32, 24, 3], [16, 12, 2]]
+    x = VEC["in/example_5d/uint16"]
+    assert x.dtype == np.uint16 and x.shape == (10, 48, 64)
+    assert int(x[3].reshape(-1)[100]) == 3100 and int(x[9].reshape(-1)[-1]) == 9000 + 3071
+    # Decimate level 1 of Z pair (0, 1): the first plane's even pixels
+    ev = VEC["ev/example_5d/uint16/decimate"]
+    out = VEC["out/example_5d/uint16/decimate"]
+    assert tuple(ev[2]) == (1, 1, 1, 32 * 24 * 2)
+    assert np.array_equal(out[:32 * 24 * 2].view(np.uint16).reshape(24, 32), x[0][::2, ::2])
 
 
 @pytest.mark.parametrize("geom,dtype,method", CASES, ids=IDS)

@@ -18,6 +18,15 @@
 //   transposed storage order (Y<->X swapped), reference: transpose_frame's
 //              per-pixel loop (array.cpp:488-504) then `sync`
 //   transposed_gpu the same on the GPU: aqz_ds_set_input_transpose + gpu_tiled
+//   async_take the patched MultiscaleArray's order with the level takes in the
+//              add's background job (aqz_ds_add_frame_async_take): add, host-
+//              tile level 0, wait, place the tiles
+// and the parts, each alone: host_tile (level 0 on the OpenMP threads),
+// h2d_pageable (add_frame_async + aqz_ds_wait_input: the upload of a
+// pageable frame), gpu_side (add_frame_async, wait, tiled takes: everything
+// but the host tiling); and, inside `async`, the host tiling's own time while
+// the upload runs beside it (async_phases: tile, then the wait that is left,
+// then the takes).  bench.py runs this binary for its e2e.caller_cpp entry.
 //
 // Build: make -C acquire-zarr_amd probe   (hipcc -fopenmp, links the library)
 #include "aqz_downsampler.h"
@@ -193,6 +202,22 @@ main(int argc, char** argv)
             lat[0].place_tiles(tile_buf[0].data(), flag_buf[0].data(), id);
     };
 
+    // async_take: every level taken tiled in the add's background job
+    std::vector<aqz_level_take> takes(NL);
+    for (uint32_t l = 1; l < NL; ++l) {
+        takes[l].mode = AQZ_TAKE_INTO;
+        takes[l].tile_rows = lat[l].tile_rows;
+        takes[l].tile_cols = lat[l].tile_cols;
+        takes[l].dst = tile_buf[l].data();
+        takes[l].cap = tile_buf[l].size();
+        takes[l].tile_nonzero = flag_buf[l].data();
+    }
+    auto place_taken = [&](uint64_t id) {
+        for (uint32_t l = 1; l < NL; ++l)
+            if (takes[l].has_frame)
+                lat[l].place_tiles(tile_buf[l].data(), flag_buf[l].data(), id);
+    };
+
     auto run = [&](const char* name, int n, auto&& step) {
         for (int i = 0; i < 2; ++i) // warm-up: first-touch of every buffer
             step(host[i % 8].data(), uint64_t(i));
@@ -214,10 +239,38 @@ main(int argc, char** argv)
         check(aqz_ds_add_frame(ds, f, fbytes), "add_frame", ds);
         take_levels_host(id);
     });
+    double ph_tile = 0, ph_wait = 0, ph_take = 0;
+    int ph_n = 0;
     run("async", frames, [&](const uint8_t* f, uint64_t id) {
+        const auto t0 = clk::now();
         check(aqz_ds_add_frame_async(ds, f, fbytes), "add_frame_async", ds);
         lat[0].host_tile(f, id); // overlaps the upload and the pyramid
-        take_levels_tiled(id);   // settles the pending add first
+        const auto t1 = clk::now();
+        check(aqz_ds_wait(ds), "wait", ds);
+        const auto t2 = clk::now();
+        take_levels_tiled(id);
+        const auto t3 = clk::now();
+        ph_tile += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        ph_wait += std::chrono::duration<double, std::milli>(t2 - t1).count();
+        ph_take += std::chrono::duration<double, std::milli>(t3 - t2).count();
+        ++ph_n;
+    });
+    run("async_take", frames, [&](const uint8_t* f, uint64_t id) {
+        check(aqz_ds_add_frame_async_take(ds, f, fbytes, takes.data()), "add_frame_async_take",
+              ds);
+        lat[0].host_tile(f, id);
+        check(aqz_ds_wait(ds), "wait", ds);
+        place_taken(id);
+    });
+    run("host_tile", frames, [&](const uint8_t* f, uint64_t id) { lat[0].host_tile(f, id); });
+    run("h2d_pageable", frames, [&](const uint8_t* f, uint64_t) {
+        check(aqz_ds_add_frame_async(ds, f, fbytes), "add_frame_async", ds);
+        check(aqz_ds_wait_input(ds), "wait_input", ds);
+        check(aqz_ds_wait(ds), "wait", ds);
+    });
+    run("gpu_side", frames, [&](const uint8_t* f, uint64_t id) {
+        check(aqz_ds_add_frame_async(ds, f, fbytes), "add_frame_async", ds);
+        take_levels_tiled(id);
     });
     run("gpu_tiled", frames, [&](const uint8_t* f, uint64_t id) {
         check(aqz_ds_add_frame_async(ds, f, fbytes), "add_frame_async", ds);
@@ -237,7 +290,10 @@ main(int argc, char** argv)
         take_input_tiled(id);
         take_levels_tiled(id);
     });
-    std::printf("}}\n");
+    std::printf("}, \"async_phases_ms\": {\"add_and_host_tile\": %.3f, \"wait_after_tile\": %.3f, "
+                "\"takes\": %.3f}}\n",
+                ph_tile / (ph_n ? ph_n : 1), ph_wait / (ph_n ? ph_n : 1),
+                ph_take / (ph_n ? ph_n : 1));
     aqz_ds_destroy(ds);
     return 0;
 }
