@@ -353,7 +353,8 @@ shift_down(uint64_t (&q)[LB / 8], uint32_t bytes)
 // and the edge path costs the interior path no registers.
 template<typename T, int E, bool NT, bool EDGE>
 __device__ __forceinline__ void
-load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tail_safe)
+load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tail_safe,
+           const T* safe)
 {
     constexpr int LB = E * int(sizeof(T));
     static_assert(LB == 16 || LB == 8, "fused loads are 8 or 16 bytes");
@@ -365,6 +366,30 @@ load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tai
             at = W - E;
     }
     uint64_t q[LB / 8] = {};
+#ifdef AQZ_EDGE_LOAD_SELECT
+    // probe variant (tools/divergent): every lane loads, from `safe` (the
+    // frame's first elements) where its chunk is out of range, and the value
+    // is selected — no exec-masked load
+    if constexpr (EDGE) {
+        const T* a0 = ok ? row + at : safe;
+        uint64_t w[LB / 8];
+        if constexpr (LB == 16) {
+            const u32x4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(a0))
+                               : *reinterpret_cast<const u32x4_u*>(a0);
+            __builtin_memcpy(w, &v, 16);
+        } else {
+            w[0] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u64_u*>(a0))
+                      : *reinterpret_cast<const u64_u*>(a0);
+        }
+#pragma unroll
+        for (int i = 0; i < LB / 8; ++i)
+            q[i] = ok ? w[i] : 0ull;
+        shift_down<LB>(q, (col - at) * uint32_t(sizeof(T)));
+        __builtin_memcpy(out, q, LB);
+        return;
+    }
+#endif
+    (void)safe;
     if (ok) {
         // explicit byte-aligned pointer types (a template argument would drop
         // the typedef's alignment)
@@ -377,6 +402,19 @@ load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tai
             q[0] = NT ? __builtin_nontemporal_load(a) : *a;
         }
     }
+#ifdef AQZ_EDGE_DEBUG
+    // probe variant (tools/divergent): report in-range edge chunks that
+    // loaded as all-zero bits (the round-5 failure's signature)
+    if constexpr (EDGE) {
+        bool zero = true;
+#pragma unroll
+        for (int i = 0; i < LB / 8; ++i)
+            zero = zero && q[i] == 0;
+        if (ok && zero)
+            printf("AQZDBG blk %u lane %u row %p col %u at %u W %u tail %d\n", blockIdx.x,
+                   threadIdx.x, (const void*)row, col, at, W, int(tail_safe));
+    }
+#endif
     if constexpr (EDGE)
         shift_down<LB>(q, (col - at) * uint32_t(sizeof(T)));
     __builtin_memcpy(out, q, LB);
@@ -1099,7 +1137,7 @@ cascade_unit(const CascadeParams& p,
             for (int k = 0; k < 2; ++k) {
                 load_chunk<T, E, NT, EDGE>(&h[k][r][0], src + uint64_t(row0 + r) * p.W,
                                            wc0 + uint32_t(k) * 64u * E + uint32_t(lane) * E, p.W,
-                                           row0 + r < p.H, !last_frame || row0 + r + 1 < p.H);
+                                           row0 + r < p.H, !last_frame || row0 + r + 1 < p.H, src);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1122,7 +1160,7 @@ cascade_unit(const CascadeParams& p,
         for (int k = 0; k < V; ++k) {
             load_chunk<T, E, NT, EDGE>(&v[r][k * E], src + uint64_t(row0 + r) * p.W,
                                        col0 + uint32_t(k) * E, p.W, row0 + r < p.H,
-                                       !last_frame || row0 + r + 1 < p.H);
+                                       !last_frame || row0 + r + 1 < p.H, src);
         }
     }
     // keep every load above the reductions (the scheduler would otherwise
@@ -1582,7 +1620,8 @@ volume_load(const VolumeParams& p,
                 load_chunk<T, E, NTL, EDGE>(&v[z][r][k * E], src + uint64_t(row0 + r) * p.W,
                                             col0 + uint32_t(k) * E, p.W, row0 + r < p.H,
                                             !(last_group && z == Z - 1) ||
-                                              row0 + r + 1 < p.H);
+                                              row0 + r + 1 < p.H,
+                                            src);
             }
         }
     }
@@ -2893,7 +2932,10 @@ AQZ_SHARDED(launch_volume)(int dtype,
         return with_method(method, [&](auto mtag) -> hipError_t {
             constexpr int M = decltype(mtag)::value;
             const bool ntl = nt_env >= 0 ? nt_env != 0 : true;
-            const int upw = M == kDecimate ? (upw_env > 0 ? std::min(upw_env, 2) : 2) : 1;
+            // $AQZ_VOLUME_UPW=4 (A/B, Decimate, nontemporal loads): four
+            // units per wave, 16 KiB of loads in flight per wave
+            const int upw = M == kDecimate ? (upw_env >= 4 ? 4 : upw_env > 0 ? std::min(upw_env, 2) : 2)
+                                           : 1;
             const uint32_t grid = grid_for((total + upw - 1) / upw, 4, 0);
 #define AQZ_VOL(NL, NTL, UPW)                                                          \
     hipLaunchKernelGGL((volume_kernel<T, M, NL, NTL, UPW>), dim3(grid), dim3(256), 0, \
@@ -2909,6 +2951,20 @@ AQZ_SHARDED(launch_volume)(int dtype,
             static const int zf_env = int_env("AQZ_VOLUME_ZFAST", -1);
             const bool zfast = zf_env >= 0 ? zf_env != 0 : (n_planes >> n_out) >= 128;
             if constexpr (M == kDecimate) {
+                if (upw == 4 && ntl) {
+                    constexpr int CZ = 16 / int(sizeof(T));
+                    if (zfast && n_out == 1)
+                        hipLaunchKernelGGL((volume_kernel<T, M, 1, true, 4, CZ, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                    else if (zfast)
+                        hipLaunchKernelGGL((volume_kernel<T, M, 2, true, 4, CZ, true>), dim3(grid),
+                                           dim3(256), 0, stream, p);
+                    else if (n_out == 1)
+                        AQZ_VOL(1, true, 4);
+                    else
+                        AQZ_VOL(2, true, 4);
+                    return hipGetLastError();
+                }
                 if (upw == 2 && zfast && ntl) {
                     constexpr int CZ = 16 / int(sizeof(T));
                     if (n_out == 1)

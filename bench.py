@@ -1363,6 +1363,8 @@ def measure_async_overlap(device, frames=24):
             "async_take_over_ideal": round(ms["async_take"] / ideal, 3),
             "async_phases_ms": d["async_phases_ms"],
             "gpu_tiled_ms_per_frame": ms["gpu_tiled"],
+            "async_one_thread_fewer_ms_per_frame": ms.get("async_one_thread_fewer"),
+            "host_tile_one_thread_fewer_ms_per_frame": ms.get("host_tile_one_thread_fewer"),
             "omp_threads": d["omp_threads"], "frames": frames,
             "path": "tools/write_frame_probe (C++ caller, OpenMP level-0 chunking): "
                     "add_frame_async; level 0 chunked on the host; wait; tiled takes"}

@@ -21,11 +21,10 @@ def rows(d):
 
 
 def short(k):
-    k = k.split("(")[0]
     for tag in ("volume_kernel", "cascade_band_kernel", "cascade_kernel", "rows_kernel", "mix_kernel"):
         if tag in k:
             return tag
-    return k[-40:]
+    return k.split("(")[0][-40:]
 
 
 for d in sorted(glob.glob(os.path.join(out, "*"))):
@@ -59,3 +58,30 @@ for d in sorted(glob.glob(os.path.join(out, "*"))):
             print(f"{name:14s} {key[0]:20s} grid {key[1]:>10s} x{n:<3d} rdreq {req:12.0f} "
                   f"wait/req {lvl / req:7.1f} cyc  stall/req {stall / req:6.3f}  "
                   f"in-flight/chan {lvl / cyc * 1.0 if cyc else 0:6.2f}  cyc {cyc:.3g}")
+
+
+def probe_cases(d):
+    """lat_probe: tools/pitch_probe.py --set volume runs, per case in
+    volume_cases() order, nt x (16:5 mix, read-only) x (3 warm + reps)
+    dispatches; the per-case means (both mixes) of the counters above."""
+    import csv as _csv
+    names = [f"plane{w}_{k}" for w in (512, 1024, 2048, 4096) for k in ("all_rows", "decimate")]
+    per = collections.OrderedDict()
+    for r in rows(d):
+        if "rows_kernel" not in r["Kernel_Name"]:
+            continue
+        per.setdefault(int(r["Dispatch_Id"]), {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    disp = list(per.values())
+    n = len(disp) // len(names)
+    for i, name in enumerate(names):
+        for half, load in ((0, "nt"), (1, "plain")):
+            g = disp[i * n + half * n // 2: i * n + (half + 1) * n // 2]
+            req = sum(x["TCC_EA0_RDREQ_sum"] for x in g) / len(g)
+            lvl = sum(x["TCC_EA0_RDREQ_LEVEL_sum"] for x in g) / len(g)
+            st = sum(x["TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"] for x in g) / len(g)
+            print(f"probe {name:20s} {load:5s} rdreq {req:10.0f} wait/req {lvl / req:7.1f} cyc  "
+                  f"stall/req {st / req:6.3f}")
+
+
+if len(sys.argv) > 2 and sys.argv[2] == "--probe-cases":
+    probe_cases(os.path.join(out, "lat_probe"))

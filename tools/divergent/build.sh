@@ -5,6 +5,8 @@
 # each with one extra compiler option, into tools/divergent/lib_<name>.so.
 # The other objects are the product build's (make -C acquire-zarr_amd first).
 #   ./tools/divergent/build.sh div "" wz "-mllvm -amdgpu-waitcnt-forcezero"
+# RELINK=1 keeps an existing variant shard object and only relinks it against
+# the current product objects (after C-ABI changes).
 # Not product code: only tests/test_gpu_divergent.py and tools/narrow_dbg.py
 # load these libraries (via $AQZ_LIB_PATH).
 set -euo pipefail
@@ -12,14 +14,19 @@ ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 B=$ROOT/acquire-zarr_amd/build
 HIPFLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-function"
 INC="-I$ROOT/include -I$ROOT/acquire-zarr_amd/csrc"
+# DIVERGENT=0 builds the product's (wave-uniform) form with the extra options
+DIVFLAG="-DAQZ_NAN_FIXUP_DIVERGENT=1"
+[ "${DIVERGENT:-1}" = 0 ] && DIVFLAG=""
 pids=()
 names=()
 while [ $# -ge 2 ]; do
   name=$1; extra=$2; shift 2
   mkdir -p "$ROOT/tools/divergent/build_$name"
   (
-    /opt/rocm/bin/hipcc $HIPFLAGS $INC -DAQZ_SHARDS=8 -DAQZ_SHARD=0 -DAQZ_NAN_FIXUP_DIVERGENT=1 $extra \
-      -c "$ROOT/acquire-zarr_amd/csrc/ds_kernels.hip" -o "$ROOT/tools/divergent/build_$name/ds_kernels_s0.o"
+    if [ "${RELINK:-0}" != 1 ] || [ ! -f "$ROOT/tools/divergent/build_$name/ds_kernels_s0.o" ]; then
+      /opt/rocm/bin/hipcc $HIPFLAGS $INC -DAQZ_SHARDS=8 -DAQZ_SHARD=0 $DIVFLAG $extra \
+        -c "$ROOT/acquire-zarr_amd/csrc/ds_kernels.hip" -o "$ROOT/tools/divergent/build_$name/ds_kernels_s0.o"
+    fi
     objs=("$ROOT/tools/divergent/build_$name/ds_kernels_s0.o")
     for o in "$B"/*.o; do
       [ "$(basename "$o")" = ds_kernels_s0.o ] || objs+=("$o")

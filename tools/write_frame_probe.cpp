@@ -262,6 +262,21 @@ main(int argc, char** argv)
         check(aqz_ds_wait(ds), "wait", ds);
         place_taken(id);
     });
+    // the same overlapped order with one OpenMP thread fewer: the library's
+    // upload thread then has a core of the box's share to itself
+    const int nthreads = omp_get_max_threads();
+    if (nthreads > 1) {
+        omp_set_num_threads(nthreads - 1);
+        run("async_one_thread_fewer", frames, [&](const uint8_t* f, uint64_t id) {
+            check(aqz_ds_add_frame_async(ds, f, fbytes), "add_frame_async", ds);
+            lat[0].host_tile(f, id);
+            check(aqz_ds_wait(ds), "wait", ds);
+            take_levels_tiled(id);
+        });
+        run("host_tile_one_thread_fewer", frames,
+            [&](const uint8_t* f, uint64_t id) { lat[0].host_tile(f, id); });
+        omp_set_num_threads(nthreads);
+    }
     run("host_tile", frames, [&](const uint8_t* f, uint64_t id) { lat[0].host_tile(f, id); });
     run("h2d_pageable", frames, [&](const uint8_t* f, uint64_t) {
         check(aqz_ds_add_frame_async(ds, f, fbytes), "add_frame_async", ds);
