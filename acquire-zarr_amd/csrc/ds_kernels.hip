@@ -121,10 +121,11 @@ x86_add(T x, T y)
 
 // Whether any lane of the wave holds a NaN result.  The fix-up runs behind a
 // wave-uniform branch.  A lane-divergent one (only the NaN lanes inside) gave
-// wrong outputs in the 16-byte f32 tiles: other columns of the NaN lanes, at
-// frame edges, on 4 of 256 fuzz cases (round 5, tools/narrow_dbg.py; root
-// cause not isolated).  The uniform branch leaves the exec mask alone and
-// passes all of them.
+// wrong outputs in edge tiles of 16-byte f32 tiles on 4 of 256 fuzz cases
+// (round 5): in-range lanes read the next row's chunk as zero or stale bits.
+// Round 6 (tools/divergent/) narrowed it to the divergent
+// branch together with exec-masked edge loads (load_chunk); either one alone
+// is exact, and tests/test_gpu_divergent.py reruns round 5's launch.
 __device__ __forceinline__ bool
 wave_any(bool p)
 {
@@ -351,6 +352,14 @@ shift_down(uint64_t (&q)[LB / 8], uint32_t bytes)
 // so nothing outside the buffer is read.  Needs W >= E (cascade_fits).
 // Every lane issues one vector load either way: no divergent element loads,
 // and the edge path costs the interior path no registers.
+//
+// Out-of-range chunks (rows past the frame, columns past W) are skipped by
+// an exec-masked load and read as zero.  AQZ_EDGE_LOAD_SELECT (probe builds,
+// tools/divergent/) loads on every lane instead — from the row's last chunk,
+// or from `safe` (the frame's first elements) for rows past the frame — and
+// selects the zero afterwards.  That form cures the round-5 divergent-branch
+// build, but it gave one wrong pixel in one default fuzz
+// run, so the product keeps the masked form with its long clean record.
 template<typename T, int E, bool NT, bool EDGE>
 __device__ __forceinline__ void
 load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tail_safe,
@@ -367,11 +376,10 @@ load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tai
     }
     uint64_t q[LB / 8] = {};
 #ifdef AQZ_EDGE_LOAD_SELECT
-    // probe variant (tools/divergent): every lane loads, from `safe` (the
-    // frame's first elements) where its chunk is out of range, and the value
-    // is selected — no exec-masked load
     if constexpr (EDGE) {
-        const T* a0 = ok ? row + at : safe;
+        // past the row end: the row's last chunk, whose line the wave's last
+        // in-range lane reads anyway; past the frame's last row: `safe`
+        const T* a0 = ok ? row + at : row_ok ? row + (W - E) : safe;
         uint64_t w[LB / 8];
         if constexpr (LB == 16) {
             const u32x4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(a0))

@@ -1,0 +1,67 @@
+"""Regression guard for the round-5 edge-tile failure (DESIGN.md §12.1,
+VERDICT r5 #1).
+
+Round 5's lane-divergent NaN fix-up gave wrong Mean outputs at frame edges
+of 16-byte f32 tiles on 4 of 256 fuzz cases, but only under round 5's
+launch rules (narrow cascade tiles, misaligned bands of <= 4 tiles, whole
+misaligned bands, two units per wave).  Those rules are no longer the
+defaults, so the ordinary fuzz test cannot see the failure any more.  This
+test puts the launch back through the library's A/B environment knobs and
+runs every float Mean fuzz case (`tools/narrow_dbg.py --float-mean`) with
+the test's inputs, with the NaN payloads replaced by the default NaN, and
+with no special values at all:
+
+- the product library (wave-uniform branch, exec-masked edge loads) must
+  give byte-identical outputs;
+- the probe build `tools/divergent/lib_divsel.so` (the divergent branch over
+  edge loads issued on every lane, `AQZ_EDGE_LOAD_SELECT`), when built, must
+  too: either ingredient alone is exact.
+
+The launch knobs are read once per process (static locals in the
+launcher), so each library runs in a child process (started, not exec'd,
+from this process).  Round 5's own form (`lib_div.so`, divergent branch +
+exec-masked edge loads) fails nondeterministically and is not asserted on;
+profiles/r06/divergent*/ hold its runs.
+"""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROUND5_LAUNCH = {
+    "AQZ_CASCADE_NARROW": "1",
+    "AQZ_BAND_MIS_MAX": "4",
+    "AQZ_BAND_MIS_SEG": "0",
+    "AQZ_UNITS_PER_WAVE": "2",
+}
+
+
+def run_probe(lib):
+    env = dict(os.environ, **ROUND5_LAUNCH)
+    if lib is not None:
+        env["AQZ_LIB_PATH"] = lib
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "narrow_dbg.py"),
+                        "--float-mean"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    m = re.search(r"^TOTAL (\d+) differing outputs", r.stdout, re.M)
+    assert m, r.stdout[-2000:]
+    return int(m.group(1)), r.stdout
+
+
+def test_product_exact_under_round5_launch():
+    n, out = run_probe(None)
+    assert n == 0, "\n".join(l for l in out.splitlines() if "differing" in l and not l.endswith(": 0 differing outputs"))
+
+
+def test_divergent_branch_exact_over_product_edge_loads():
+    lib = os.path.join(ROOT, "tools", "divergent", "lib_divsel.so")
+    if not os.path.exists(lib):
+        pytest.skip("probe build absent (tools/divergent/build.sh divsel \"\")")
+    n, out = run_probe(lib)
+    assert n == 0, "\n".join(l for l in out.splitlines() if "differing" in l and not l.endswith(": 0 differing outputs"))

@@ -4,7 +4,10 @@
 # shard 0 (u8 + f32 kernels) is compiled with -DAQZ_NAN_FIXUP_DIVERGENT=1,
 # each with one extra compiler option, into tools/divergent/lib_<name>.so.
 # The other objects are the product build's (make -C acquire-zarr_amd first).
-#   ./tools/divergent/build.sh div "" wz "-mllvm -amdgpu-waitcnt-forcezero"
+#   ./tools/divergent/build.sh div "" divsel "-DAQZ_EDGE_LOAD_SELECT=1"
+# div = round 5's form (divergent branch + the product's exec-masked edge
+# loads), divsel = the divergent branch over edge loads issued on every lane
+# (DESIGN.md §12.1).
 # RELINK=1 keeps an existing variant shard object and only relinks it against
 # the current product objects (after C-ABI changes).
 # Not product code: only tests/test_gpu_divergent.py and tools/narrow_dbg.py
