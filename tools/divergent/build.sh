@@ -1,6 +1,6 @@
 #!/bin/bash
 # Regression probe for the round-5 lane-divergent NaN fix-up (VERDICT r5 #1,
-# DESIGN.md §11.6): builds variant copies of libaqz_downsampler.so whose
+# docs/HISTORY.md §11.6): builds variant copies of libaqz_downsampler.so whose
 # shard 0 (u8 + f32 kernels) is compiled with -DAQZ_NAN_FIXUP_DIVERGENT=1,
 # each with one extra compiler option, into tools/divergent/lib_<name>.so.
 # The other objects are the product build's (make -C acquire-zarr_amd first).
