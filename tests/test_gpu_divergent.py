@@ -59,9 +59,21 @@ def test_product_exact_under_round5_launch():
     assert n == 0, "\n".join(l for l in out.splitlines() if "differing" in l and not l.endswith(": 0 differing outputs"))
 
 
-def test_divergent_branch_exact_over_product_edge_loads():
+def test_divergent_branch_exact_over_select_edge_loads():
     lib = os.path.join(ROOT, "tools", "divergent", "lib_divsel.so")
     if not os.path.exists(lib):
         pytest.skip("probe build absent (tools/divergent/build.sh divsel \"\")")
     n, out = run_probe(lib)
     assert n == 0, "\n".join(l for l in out.splitlines() if "differing" in l and not l.endswith(": 0 differing outputs"))
+
+
+@pytest.mark.xfail(strict=False, reason="round 5's form (divergent NaN branch + exec-masked "
+                   "edge loads) gives wrong edge outputs under round 5's launch; the "
+                   "documented repro of DESIGN.md §12.1 (nondeterministic, so not strict)")
+def test_round5_form_documented_repro():
+    lib = os.path.join(ROOT, "tools", "divergent", "lib_div.so")
+    if not os.path.exists(lib):
+        pytest.skip("probe build absent (tools/divergent/build.sh div \"\")")
+    n, out = run_probe(lib)
+    print(f"round 5's form: {n} differing outputs")
+    assert n == 0
