@@ -6,8 +6,10 @@
  * through one handle (the expected bytes) and through aqz_node on handles
  * that repeat device 0: the host batch, the device batch in place and staged
  * (AQZ_NODE_STAGE_ALL: peer-copy staging, three streams and events), the
- * stream (add / wait_input / take / flush), and the
- * single-handle async add.  Every result is compared byte for byte with the
+ * stream (add / wait_input / take / flush), the stream as the drop-in's
+ * node mode runs it (buffers kept until aqz_node_inputs_released counts
+ * them; round 6), and the single-handle async add with
+ * aqz_ds_input_pending.  Every result is compared byte for byte with the
  * one-handle run.  Exits nonzero on the first mismatch or error.
  */
 #include <stdint.h>
@@ -136,6 +138,63 @@ run_case(const aqz_level_desc* lv, uint32_t nl, uint32_t n, int method, const ch
     for (uint32_t L = 1; L < nl; ++L)
         if (taken[L] != cref[L] || memcmp(got[L], ref[L], level_bytes(&lv[L]) * cref[L]))
             return fprintf(stderr, "%s stream L%u differs (%zu frames)\n", name, L, taken[L]), 1;
+
+    /* node stream as the drop-in's node mode runs it (round 6,
+     * Downsampler::release_frame): no wait_input; a frame's buffer is kept
+     * until aqz_node_inputs_released counts the frame, then rewritten with a
+     * later one (three buffers for three handles) */
+    {
+        enum { NB = 3 };
+        uint8_t* bufs[NB];
+        uint64_t holds[NB]; /* frame id the buffer was given, or UINT64_MAX */
+        uint64_t base = 0, released = 0;
+        CHECK(aqz_node_inputs_released(node, &base)); /* every earlier frame */
+        for (int b = 0; b < NB; ++b) {
+            bufs[b] = malloc(fb);
+            holds[b] = UINT64_MAX;
+        }
+        memset(taken, 0, sizeof taken);
+        for (uint32_t k = 0; k <= n; ++k) {
+            if (k < n) {
+                int b = -1;
+                for (long spin = 0; b < 0 && spin < 2000000; ++spin) {
+                    CHECK(aqz_node_inputs_released(node, &released));
+                    for (int i = 0; i < NB && b < 0; ++i)
+                        if (holds[i] == UINT64_MAX || holds[i] < released)
+                            b = i;
+                }
+                if (b < 0)
+                    return fprintf(stderr, "%s keep: no buffer released\n", name), 1;
+                memcpy(bufs[b], host + fb * k, fb);
+                CHECK(aqz_node_add_frame(node, bufs[b], fb));
+                holds[b] = base + k;
+            } else {
+                CHECK(aqz_node_flush(node));
+            }
+            for (uint32_t L = 1; L < nl; ++L) {
+                for (;;) {
+                    const size_t lb = level_bytes(&lv[L]);
+                    size_t nb = 0;
+                    int has = 0;
+                    if (taken[L] >= cref[L])
+                        break;
+                    CHECK(aqz_node_take_frame(node, L, got[L] + taken[L] * lb, lb, &nb, &has));
+                    if (!has)
+                        break;
+                    ++taken[L];
+                }
+            }
+        }
+        CHECK(aqz_node_inputs_released(node, &released));
+        if (released != base + n)
+            return fprintf(stderr, "%s keep: released %llu of %llu\n", name,
+                           (unsigned long long)released, (unsigned long long)(base + n)), 1;
+        for (int b = 0; b < NB; ++b)
+            free(bufs[b]);
+        for (uint32_t L = 1; L < nl; ++L)
+            if (taken[L] != cref[L] || memcmp(got[L], ref[L], level_bytes(&lv[L]) * cref[L]))
+                return fprintf(stderr, "%s keep L%u differs (%zu frames)\n", name, L, taken[L]), 1;
+    }
     aqz_node_destroy(node);
 
     /* single handle, async add + wait_input + take */
@@ -143,7 +202,14 @@ run_case(const aqz_level_desc* lv, uint32_t nl, uint32_t n, int method, const ch
     size_t taken1[MAXL] = { 0 };
     for (uint32_t k = 0; k < n; ++k) {
         CHECK(aqz_ds_add_frame_async(ds, host + fb * k, fb));
+        int pend = -1;
+        CHECK(aqz_ds_input_pending(ds, &pend)); /* 0 or 1, either is right here */
+        if (pend != 0 && pend != 1)
+            return fprintf(stderr, "%s input_pending %d\n", name, pend), 1;
         CHECK(aqz_ds_wait_input(ds));
+        CHECK(aqz_ds_input_pending(ds, &pend));
+        if (pend != 0)
+            return fprintf(stderr, "%s input still pending after wait_input\n", name), 1;
         CHECK(aqz_ds_wait(ds));
         for (uint32_t L = 1; L < nl; ++L) {
             const size_t lb = level_bytes(&lv[L]);
