@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 for v in product product product masked masked; do
   lib=$PWD/acquire-zarr_amd/libaqz_downsampler.so
   [ $v = masked ] && lib=$PWD/tools/divergent/lib_masked.so
-  AQZ_LIB_PATH=$lib timeout -k 10 300 python -u tools/narrow_dbg.py --cases 181,153,25,51 >> $OUT/dbg_$v.log 2>&1
+  AQZ_LIB_PATH=$lib timeout -k 10 300 python -u tests/narrow_dbg.py --cases 181,153,25,51 >> $OUT/dbg_$v.log 2>&1
   rc=$?
   echo "== $v rc=$rc"; grep -E "differing|TOTAL" $OUT/dbg_$v.log | tail -4
   [ $rc -eq 0 ] || exit $rc

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: the round-5 lane-divergent NaN fix-up (tools/divergent/build.sh)
 # under compiler switches that isolate the failing pass; the fuzz suite and
-# the per-output dump (tools/narrow_dbg.py) for each variant.
+# the per-output dump (tests/narrow_dbg.py) for each variant.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT=gpurun_out/r06_divergent; mkdir -p $OUT
@@ -14,7 +14,7 @@ for v in div wz; do
   echo "$v: rc=$rc $(tail -1 $OUT/fuzz_$v.log)"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 done
-AQZ_LIB_PATH=$PWD/tools/divergent/lib_div.so timeout -k 10 300 python -u tools/narrow_dbg.py > $OUT/dbg_div.log 2>&1 || exit $?
+AQZ_LIB_PATH=$PWD/tools/divergent/lib_div.so timeout -k 10 300 python -u tests/narrow_dbg.py > $OUT/dbg_div.log 2>&1 || exit $?
 grep "differing" $OUT/dbg_div.log || true
 timeout -k 10 600 python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu \
   tests/test_gpu_reference_vectors.py tests/test_gpu_adapter.py -k "example" > $OUT/example.log 2>&1

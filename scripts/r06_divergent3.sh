@@ -15,7 +15,7 @@ for v in prodwz divsel divdbg product product product; do
   lib=$PWD/tools/divergent/lib_$v.so
   [ $v = product ] && lib=$PWD/acquire-zarr_amd/libaqz_downsampler.so
   [ -f $lib ] || { echo "== $v: not built"; continue; }
-  env $R5 AQZ_LIB_PATH=$lib timeout -k 10 300 python -u tools/narrow_dbg.py >> $OUT/dbg_$v.log 2>&1
+  env $R5 AQZ_LIB_PATH=$lib timeout -k 10 300 python -u tests/narrow_dbg.py >> $OUT/dbg_$v.log 2>&1
   rc=$?
   echo "== $v rc=$rc"; grep "differing" $OUT/dbg_$v.log | tail -12
   [ $rc -eq 0 ] || exit $rc

@@ -14,7 +14,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_divergent.py tests/test_gpu
 tail -1 $OUT/pytest.log
 if [ -f tools/divergent/lib_divdbg.so ]; then
   env AQZ_CASCADE_NARROW=1 AQZ_BAND_MIS_MAX=4 AQZ_BAND_MIS_SEG=0 AQZ_UNITS_PER_WAVE=2 \
-    AQZ_LIB_PATH=$PWD/tools/divergent/lib_divdbg.so timeout -k 10 300 python -u tools/narrow_dbg.py > $OUT/dbg_divdbg.log 2>&1
+    AQZ_LIB_PATH=$PWD/tools/divergent/lib_divdbg.so timeout -k 10 300 python -u tests/narrow_dbg.py > $OUT/dbg_divdbg.log 2>&1
   rc=$?
   echo "== divdbg rc=$rc AQZDBG lines: $(grep -c AQZDBG $OUT/dbg_divdbg.log)"
   grep "differing" $OUT/dbg_divdbg.log

@@ -23,7 +23,7 @@ for rep in 1 2 3 4; do
 done
 # the divergent build over select loads, with forced-zero waitcnts
 env AQZ_CASCADE_NARROW=1 AQZ_BAND_MIS_MAX=4 AQZ_BAND_MIS_SEG=0 AQZ_UNITS_PER_WAVE=2 \
-  AQZ_LIB_PATH=$PWD/tools/divergent/lib_divselwz.so timeout -k 10 300 python -u tools/narrow_dbg.py --float-mean \
+  AQZ_LIB_PATH=$PWD/tools/divergent/lib_divselwz.so timeout -k 10 300 python -u tests/narrow_dbg.py --float-mean \
   > $OUT/dbg_divselwz.log 2>&1 || exit $?
 echo "divselwz: $(tail -1 $OUT/dbg_divselwz.log)"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_divergent.py -v --timeout 300 --timeout-method thread \

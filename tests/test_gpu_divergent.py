@@ -7,7 +7,7 @@ launch rules (narrow cascade tiles, misaligned bands of <= 4 tiles, whole
 misaligned bands, two units per wave).  Those rules are no longer the
 defaults, so the ordinary fuzz test cannot see the failure any more.  This
 test puts the launch back through the library's A/B environment knobs and
-runs every float Mean fuzz case (`tools/narrow_dbg.py --float-mean`) with
+runs every float Mean fuzz case (`tests/narrow_dbg.py --float-mean`) with
 the test's inputs, with the NaN payloads replaced by the default NaN, and
 with no special values at all:
 
@@ -45,7 +45,7 @@ def run_probe(lib):
     env = dict(os.environ, **ROUND5_LAUNCH)
     if lib is not None:
         env["AQZ_LIB_PATH"] = lib
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "narrow_dbg.py"),
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "narrow_dbg.py"),
                         "--float-mean"], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

@@ -10,7 +10,7 @@
 # (DESIGN.md §12.1).
 # RELINK=1 keeps an existing variant shard object and only relinks it against
 # the current product objects (after C-ABI changes).
-# Not product code: only tests/test_gpu_divergent.py and tools/narrow_dbg.py
+# Not product code: only tests/test_gpu_divergent.py and tests/narrow_dbg.py
 # load these libraries (via $AQZ_LIB_PATH).
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
