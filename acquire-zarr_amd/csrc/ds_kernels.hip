@@ -319,12 +319,72 @@ store_vec(T* dst, const T (&v)[N])
     }
 }
 
+#ifdef AQZ_EDGE_SHIFT_ASM
+// probe variants (tools/divergent): the 64-bit shifts as
+// inline asm, =2 with two wait states after each one
+__device__ __forceinline__ uint64_t
+probe_shr64(uint64_t x, uint32_t n)
+{
+    uint64_t r;
+#if AQZ_EDGE_SHIFT_ASM == 2
+    asm volatile("v_lshrrev_b64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(n), "v"(x));
+#else
+    asm volatile("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "v"(n), "v"(x));
+#endif
+    return r;
+}
+__device__ __forceinline__ uint64_t
+probe_shl64(uint64_t x, uint32_t n)
+{
+    uint64_t r;
+#if AQZ_EDGE_SHIFT_ASM == 2
+    asm volatile("v_lshlrev_b64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(n), "v"(x));
+#else
+    asm volatile("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "v"(n), "v"(x));
+#endif
+    return r;
+}
+#endif
+
 // Shift a little-endian LB-byte vector down by `bytes` (0 <= bytes < LB).
 template<int LB>
 __device__ __forceinline__ void
 shift_down(uint64_t (&q)[LB / 8], uint32_t bytes)
 {
+#ifdef AQZ_EDGE_SHIFT32
+    // probe variant (tools/divergent): the same shift in
+    // 32-bit words, no 64-bit shifts; `bytes` >= LB gives zero
+    if constexpr (LB == 16) {
+        uint32_t w[4], o[4];
+        __builtin_memcpy(w, q, 16);
+        const uint32_t k = bytes >> 2, r = (bytes & 3u) * 8u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t j = uint32_t(i) + k;
+            const uint32_t a = j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : j == 3 ? w[3] : 0u;
+            const uint32_t b = j == 0 ? w[1] : j == 1 ? w[2] : j == 2 ? w[3] : 0u;
+            o[i] = r ? (a >> r) | (b << (32u - r)) : a;
+        }
+        __builtin_memcpy(q, o, 16);
+        return;
+    }
+#endif
     const uint32_t n = 8 * bytes;
+#ifdef AQZ_EDGE_SHIFT_ASM
+    if constexpr (LB == 16) {
+        uint64_t lo = q[0], hi = q[1];
+        if (n >= 64) {
+            lo = probe_shr64(hi, n - 64);
+            hi = 0;
+        } else if (n) {
+            lo = probe_shr64(lo, n) | probe_shl64(hi, 64 - n);
+            hi = probe_shr64(hi, n);
+        }
+        q[0] = lo;
+        q[1] = hi;
+        return;
+    }
+#endif
     if constexpr (LB == 8) {
         q[0] = n ? q[0] >> n : q[0];
     } else {
@@ -378,8 +438,9 @@ load_chunk(T* out, const T* row, uint32_t col, uint32_t W, bool row_ok, bool tai
 #ifdef AQZ_EDGE_LOAD_SELECT
     if constexpr (EDGE) {
         // past the row end: the row's last chunk, whose line the wave's last
-        // in-range lane reads anyway; past the frame's last row: `safe`
-        const T* a0 = ok ? row + at : row_ok ? row + (W - E) : safe;
+        // in-range lane reads anyway (=1), or `safe` (=2); past the frame's
+        // last row: `safe`
+        const T* a0 = ok ? row + at : (row_ok && AQZ_EDGE_LOAD_SELECT == 1) ? row + (W - E) : safe;
         uint64_t w[LB / 8];
         if constexpr (LB == 16) {
             const u32x4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(a0))

@@ -20,19 +20,21 @@ INC="-I$ROOT/include -I$ROOT/acquire-zarr_amd/csrc"
 # DIVERGENT=0 builds the product's (wave-uniform) form with the extra options
 DIVFLAG="-DAQZ_NAN_FIXUP_DIVERGENT=1"
 [ "${DIVERGENT:-1}" = 0 ] && DIVFLAG=""
+# SHARD=k: vary dtype shard k instead of 0 (1 holds the u16 kernels)
+SHARD=${SHARD:-0}
 pids=()
 names=()
 while [ $# -ge 2 ]; do
   name=$1; extra=$2; shift 2
   mkdir -p "$ROOT/tools/divergent/build_$name"
   (
-    if [ "${RELINK:-0}" != 1 ] || [ ! -f "$ROOT/tools/divergent/build_$name/ds_kernels_s0.o" ]; then
-      /opt/rocm/bin/hipcc $HIPFLAGS $INC -DAQZ_SHARDS=8 -DAQZ_SHARD=0 $DIVFLAG $extra \
-        -c "$ROOT/acquire-zarr_amd/csrc/ds_kernels.hip" -o "$ROOT/tools/divergent/build_$name/ds_kernels_s0.o"
+    if [ "${RELINK:-0}" != 1 ] || [ ! -f "$ROOT/tools/divergent/build_$name/ds_kernels_s$SHARD.o" ]; then
+      /opt/rocm/bin/hipcc $HIPFLAGS $INC -DAQZ_SHARDS=8 -DAQZ_SHARD=$SHARD $DIVFLAG $extra \
+        -c "$ROOT/acquire-zarr_amd/csrc/ds_kernels.hip" -o "$ROOT/tools/divergent/build_$name/ds_kernels_s$SHARD.o"
     fi
-    objs=("$ROOT/tools/divergent/build_$name/ds_kernels_s0.o")
+    objs=("$ROOT/tools/divergent/build_$name/ds_kernels_s$SHARD.o")
     for o in "$B"/*.o; do
-      [ "$(basename "$o")" = ds_kernels_s0.o ] || objs+=("$o")
+      [ "$(basename "$o")" = ds_kernels_s$SHARD.o ] || objs+=("$o")
     done
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/divergent/lib_$name.so" \
       "${objs[@]}" -Wl,-rpath,/opt/rocm/lib -ldl -lpthread
