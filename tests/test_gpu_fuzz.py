@@ -12,6 +12,7 @@ input and output buffers at element-aligned but otherwise arbitrary byte
 offsets (which turns aligned rows into misaligned ones).  Integers bit-exact,
 floats within 1 ulp (assert_parity).  Also: chunk-tiled batches with random
 tile shapes, and Z stacks (fused 2x2x2 or the Z state machine)."""
+import os
 import re
 import zlib
 
@@ -25,7 +26,8 @@ pytestmark = pytest.mark.gpu
 
 DTYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16,
           np.int32, np.int64, np.float32, np.float64]
-N_CASES = 256
+# $AQZ_FUZZ_CASES widens the sweep for one-off runs (scripts/r06_fuzzwide.sh)
+N_CASES = int(os.environ.get("AQZ_FUZZ_CASES", "256"))
 
 
 def case_params(i):
