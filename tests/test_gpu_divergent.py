@@ -15,7 +15,11 @@ with no special values at all:
   give byte-identical outputs;
 - the probe build `tools/divergent/lib_divsel.so` (the divergent branch over
   edge loads issued on every lane, `AQZ_EDGE_LOAD_SELECT`), when built, must
-  too: either ingredient alone is exact.
+  too: either ingredient alone is exact;
+- so must `tools/divergent/lib_divnolr.so`: round 5's form itself, built
+  with LLVM's VGPR live-range optimisation for if-else regions off
+  (`-mllvm -amdgpu-opt-vgpr-liverange=false`), the pass the failure is
+  traced to.
 
 The launch knobs are read once per process (static locals in the
 launcher), so each library runs in a child process (started, not exec'd,
@@ -63,6 +67,18 @@ def test_divergent_branch_exact_over_select_edge_loads():
     lib = os.path.join(ROOT, "tools", "divergent", "lib_divsel.so")
     if not os.path.exists(lib):
         pytest.skip("probe build absent (tools/divergent/build.sh divsel \"\")")
+    n, out = run_probe(lib)
+    assert n == 0, "\n".join(l for l in out.splitlines() if "differing" in l and not l.endswith(": 0 differing outputs"))
+
+
+def test_divergent_branch_exact_without_vgpr_liverange_opt():
+    """The cause: round 5's form built with LLVM's VGPR
+    live-range optimisation for if-else regions off
+    (-mllvm -amdgpu-opt-vgpr-liverange=false) is exact."""
+    lib = os.path.join(ROOT, "tools", "divergent", "lib_divnolr.so")
+    if not os.path.exists(lib):
+        pytest.skip("probe build absent (tools/divergent/build.sh divnolr "
+                    "\"-mllvm -amdgpu-opt-vgpr-liverange=false\")")
     n, out = run_probe(lib)
     assert n == 0, "\n".join(l for l in out.splitlines() if "differing" in l and not l.endswith(": 0 differing outputs"))
 
